@@ -1,0 +1,668 @@
+// rt_render.hip — the MI355X (gfx950) render kernel and the C-ABI of include/rt_mi355x.h.
+//
+// One work-item per pixel; a wave covers an 8x8 pixel tile (coherent rays), a 256-thread
+// workgroup a 16x16 tile.  Per pixel the kernel runs trace_ray_through_pixel/3
+// (raytracer.erl:180-184) and everything below it, in IEEE binary64 with the
+// reference's operation order and no contraction (-ffp-contract=off + the pragma
+// below): the geometry (every hit/miss decision, every hit point and normal) is
+// bit-identical to the reference; colours differ from libm only where device pow()
+// differs from the host's by an ulp.
+//
+// Work per hit level (the reference's recursion, raytracer.erl:186-252):
+//   * one nearest-object scan (nearest_object_intersecting_ray/6, :303-346) — objects are
+//     grouped by type, each type a wave-uniform loop reading its records with scalar
+//     loads (uniform index -> s_load into SGPRs, the FP64 VALU reads them directly);
+//   * per point light, diffuse + specular shading and one shadow test
+//     (shadow_factor/4, :256-267).  The reference's test is "the nearest object seen
+//     from the light is the hit object"; it is restated exactly as a bounded any-hit
+//     test: with t* = the hit object's own distance along the shadow ray, the light is
+//     blocked iff some object has a valid hit with t < t*, or t == t* and an earlier list
+//     position.  That lets a lane stop at the first blocker and the wave leave the loop
+//     as soon as every lane is decided (a wave-wide ballot).
+// The reflection the reference recomputes once per light (:216-224) is the same value
+// every time; it is computed once (ORDER_EXACT keeps the reference's summation order by
+// shading the chain backwards from its deepest hit; ORDER_FAST accumulates forwards).
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/rt_mi355x.h"
+#include "rt_layout.h"
+#include "rt_scene.h"
+
+using namespace rtl;
+
+namespace {
+
+constexpr int BLOCK = 256; // 4 waves, 16x16 pixels
+constexpr int TILE = 16;
+
+struct D3 {
+    double x, y, z;
+};
+
+__device__ __forceinline__ double dot3(const D3 &a, const D3 &b) { // vector_dot_product/2 (:546-547)
+    return a.x * b.x + a.y * b.y + a.z * b.z;
+}
+
+__device__ __forceinline__ D3 normalize3(const D3 &v) { // vector_normalize/1 (:554-560)
+    double mag = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+    double s = 1.0 / mag;
+    D3 r = {v.x * s, v.y * s, v.z * s};
+    if (mag == 0) r = D3{0.0, 0.0, 0.0};
+    return r;
+}
+
+__device__ __forceinline__ D3 bounce3(const D3 &v, const D3 &n) { // vector_bounce_off_plane/2 (:568-573)
+    double k = 2 * (n.x * -v.x + n.y * -v.y + n.z * -v.z);
+    return D3{n.x * k + v.x, n.y * k + v.y, n.z * k + v.z};
+}
+
+__device__ __forceinline__ double max0(double x) { return x > 0 ? x : 0.0; } // lists:max([0, X])
+
+// ---- primitive tests: return true and t on a valid hit --------------------------------------
+// ray_sphere_intersect/2 (:364-397), from B and C (A4 = 4*A hoisted per ray)
+__device__ __forceinline__ bool sph_t(double B, double C, double A4, double &t) {
+    double disc = B * B - A4 * C;
+    if (!(disc >= 0.001)) return false;
+    double sq = sqrt(disc);
+    double t0 = (-B + sq) / 2;
+    double t1 = (-B - sq) / 2;
+    if (!((t0 >= 0) && (t1 >= 0))) return false;
+    t = (t1 < t0) ? t1 : t0; // lists:min([T0, T1])
+    return true;
+}
+
+// ray_triangle_intersect/2 (:402-455), with T = O - v1 and Q = T x Edge1 given
+__device__ __forceinline__ bool tri_t(const D3 &d, const D3 &e1, const D3 &e2, const D3 &T, const D3 &Q,
+                                      double &t) {
+    D3 P = {d.y * e2.z - d.z * e2.y, d.z * e2.x - d.x * e2.z, d.x * e2.y - d.y * e2.x};
+    double det = dot3(e1, P);
+    if (det < 0.000001) return false;
+    double U = dot3(T, P);
+    if ((U < 0) || (U > det)) return false;
+    double V = dot3(d, Q);
+    if ((V < 0) || (U + V > det)) return false;
+    t = dot3(e2, Q) / det;
+    return true;
+}
+
+// ray_plane_intersect/2 (:461-480), with V0 = -(N.O + Distance) given
+__device__ __forceinline__ bool pl_t(const D3 &n, const D3 &d, double V0, double &t) {
+    double Vd = dot3(n, d);
+    if (!(Vd < 0)) return false;
+    t = V0 / Vd;
+    if (t < 0.001) return false;
+    return true;
+}
+
+__device__ __forceinline__ bool nearer(double t, int id, double bt, int bid) {
+    return t < bt || (t == bt && id < bid); // first in list order among equal distances (:319)
+}
+
+struct Scene {
+    SceneHdr h;
+    const double *__restrict__ tab;
+    const int *__restrict__ itab;
+};
+
+// nearest_object_intersecting_ray/6 (:303-346).  PRE: the ray starts at origin slot `org`
+// (tabled); otherwise at r_o.  Returns the compact object id (-1 = none) and its t.
+template <bool PRE>
+__device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt) {
+    const SceneHdr &h = S.h;
+    bt = __builtin_inf();
+    int bid = 0x7fffffff;
+    const double A4 = 4 * (d.x * d.x + d.y * d.y + d.z * d.z);
+    for (int k = 0; k < h.n_sph; ++k) {
+        double B, C;
+        if (PRE) {
+            const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
+            B = 2 * (d.x * q[0] + d.y * q[1] + d.z * q[2]);
+            C = q[3];
+        } else {
+            const double *s = S.tab + h.o_sph + k * SPH_W;
+            D3 oc = {o.x - s[0], o.y - s[1], o.z - s[2]};
+            B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
+            C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - s[3];
+        }
+        double t;
+        if (sph_t(B, C, A4, t)) {
+            int id = S.itab[h.i_sph_id + k];
+            if (nearer(t, id, bt, bid)) { bt = t; bid = id; }
+        }
+    }
+    for (int k = 0; k < h.n_tri; ++k) {
+        const double *g = S.tab + h.o_tri + k * TRI_W;
+        D3 e1 = {g[3], g[4], g[5]}, e2 = {g[6], g[7], g[8]};
+        D3 T, Q;
+        if (PRE) {
+            const double *q = S.tab + h.o_tri_org + (org * h.n_tri + k) * TRI_ORG_W;
+            T = D3{q[0], q[1], q[2]};
+            Q = D3{q[3], q[4], q[5]};
+        } else {
+            T = D3{o.x - g[0], o.y - g[1], o.z - g[2]};
+            Q = D3{T.y * e1.z - T.z * e1.y, T.z * e1.x - T.x * e1.z, T.x * e1.y - T.y * e1.x};
+        }
+        double t;
+        if (tri_t(d, e1, e2, T, Q, t)) {
+            int id = S.itab[h.i_tri_id + k];
+            if (nearer(t, id, bt, bid)) { bt = t; bid = id; }
+        }
+    }
+    for (int k = 0; k < h.n_pl; ++k) {
+        const double *p = S.tab + h.o_pl + k * PL_W;
+        D3 n = {p[0], p[1], p[2]};
+        double V0 = PRE ? S.tab[h.o_pl_org + org * h.n_pl + k] : -(n.x * o.x + n.y * o.y + n.z * o.z + p[3]);
+        double t;
+        if (pl_t(n, d, V0, t)) {
+            int id = S.itab[h.i_pl_id + k];
+            if (nearer(t, id, bt, bid)) { bt = t; bid = id; }
+        }
+    }
+    return bid == 0x7fffffff ? -1 : bid;
+}
+
+// Hit point and normal of object `id` at distance t (as computed inside the reference's
+// intersect functions: Intersection = O + D*t, :384-390, :443-451, :471-476).
+__device__ __forceinline__ void hit_geom(const Scene &S, int id, const D3 &o, const D3 &d, double t, D3 &hit,
+                                         D3 &N) {
+    hit = D3{o.x + d.x * t, o.y + d.y * t, o.z + d.z * t};
+    const double *r = S.tab + S.h.o_obj + id * OBJ_W;
+    int kind = S.itab[S.h.i_obj_meta + id * OBJ_META_W];
+    if (kind == K_SPHERE)
+        N = normalize3(D3{hit.x - r[0], hit.y - r[1], hit.z - r[2]});
+    else
+        N = D3{r[0], r[1], r[2]};
+}
+
+// shadow_factor/4 (:256-267) as the exact bounded any-hit test described at the top.
+// c = canonical compact id of the hit object, sd = normalize(Hit - Light).
+__device__ __forceinline__ bool lit_by(const Scene &S, int light, int c, const D3 &sd, bool active) {
+    const SceneHdr &h = S.h;
+    const int org = 1 + light;
+    const double A4 = 4 * (sd.x * sd.x + sd.y * sd.y + sd.z * sd.z);
+    // t* of the target itself along the shadow ray
+    double ts = 0;
+    bool valid = false;
+    if (active) {
+        const int kind = S.itab[h.i_obj_meta + c * OBJ_META_W + 0];
+        const int loc = S.itab[h.i_obj_meta + c * OBJ_META_W + 1];
+        if (kind == K_SPHERE) {
+            const double *q = S.tab + h.o_sph_org + (org * h.n_sph + loc) * SPH_ORG_W;
+            double B = 2 * (sd.x * q[0] + sd.y * q[1] + sd.z * q[2]);
+            valid = sph_t(B, q[3], A4, ts);
+        } else if (kind == K_TRIANGLE) {
+            const double *g = S.tab + h.o_tri + loc * TRI_W;
+            const double *q = S.tab + h.o_tri_org + (org * h.n_tri + loc) * TRI_ORG_W;
+            valid = tri_t(sd, D3{g[3], g[4], g[5]}, D3{g[6], g[7], g[8]}, D3{q[0], q[1], q[2]}, D3{q[3], q[4], q[5]},
+                          ts);
+        } else {
+            const double *p = S.tab + h.o_pl + loc * PL_W;
+            valid = pl_t(D3{p[0], p[1], p[2]}, sd, S.tab[h.o_pl_org + org * h.n_pl + loc], ts);
+        }
+    }
+    bool blocked = !valid; // a target the shadow ray misses is never lit
+    if (__all(blocked)) return false;
+    for (int k = 0; k < h.n_sph; ++k) {
+        if (!blocked) {
+            const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
+            double B = 2 * (sd.x * q[0] + sd.y * q[1] + sd.z * q[2]);
+            double t;
+            if (sph_t(B, q[3], A4, t)) {
+                int id = S.itab[h.i_sph_id + k];
+                blocked = t < ts || (t == ts && id < c);
+            }
+        }
+        if (__all(blocked)) return false;
+    }
+    for (int k = 0; k < h.n_tri; ++k) {
+        if (!blocked) {
+            const double *g = S.tab + h.o_tri + k * TRI_W;
+            const double *q = S.tab + h.o_tri_org + (org * h.n_tri + k) * TRI_ORG_W;
+            double t;
+            if (tri_t(sd, D3{g[3], g[4], g[5]}, D3{g[6], g[7], g[8]}, D3{q[0], q[1], q[2]}, D3{q[3], q[4], q[5]}, t)) {
+                int id = S.itab[h.i_tri_id + k];
+                blocked = t < ts || (t == ts && id < c);
+            }
+        }
+        if (__all(blocked)) return false;
+    }
+    for (int k = 0; k < h.n_pl; ++k) {
+        if (!blocked) {
+            const double *p = S.tab + h.o_pl + k * PL_W;
+            double t;
+            if (pl_t(D3{p[0], p[1], p[2]}, sd, S.tab[h.o_pl_org + org * h.n_pl + k], t)) {
+                int id = S.itab[h.i_pl_id + k];
+                blocked = t < ts || (t == ts && id < c);
+            }
+        }
+        if (__all(blocked)) return false;
+    }
+    return !blocked;
+}
+
+// lighting_function/6 (:209-252) for one hit, with the (per-light identical) reflection R.
+__device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D3 &hit, const D3 &N, const D3 &R,
+                                    bool active) {
+    const SceneHdr &h = S.h;
+    const double *m = S.tab + h.o_obj + id * OBJ_W;
+    const D3 mc = {m[3], m[4], m[5]};
+    const double spow = m[6], shin = m[7];
+    const int c = S.itab[h.i_obj_meta + id * OBJ_META_W + 2];
+    D3 F = {0.0, 0.0, 0.0};
+    for (int i = 0; i < h.n_light; ++i) {
+        const double *L = S.tab + h.o_light + i * LIGHT_W;
+        const D3 Lc = {L[0], L[1], L[2]}, Lp = {L[3], L[4], L[5]}, Sc = {L[6], L[7], L[8]};
+        // diffuse_term/4 (:272-279)
+        const D3 ln = normalize3(D3{Lp.x - hit.x, Lp.y - hit.y, Lp.z - hit.z});
+        const double dd = max0(dot3(N, ln));
+        const D3 diff = {mc.x * dd, mc.y * dd, mc.z * dd};
+        // specular_term/7 (:285-297)
+        const D3 hn = normalize3(D3{ln.x + -d.x, ln.y + -d.y, ln.z + -d.z});
+        const double sp = shin * pow(max0(dot3(hn, N)), spow);
+        const D3 spec = {Sc.x * sp, Sc.y * sp, Sc.z * sp};
+        const D3 con = {diff.x + spec.x, diff.y + spec.y, diff.z + spec.z};
+        // shadow ray direction normalize(Hit - Light) == -normalize(Light - Hit), bit for bit
+        const double lit = lit_by(S, i, c, D3{-ln.x, -ln.y, -ln.z}, active) ? 1.0 : 0.0;
+        F.x = F.x + (R.x + Lc.x * con.x * lit);
+        F.y = F.y + (R.y + Lc.y * con.y * lit);
+        F.z = F.z + (R.z + Lc.z * con.z * lit);
+    }
+    return F;
+}
+
+template <int ORDER, int PREC, bool LEVELS>
+__global__ __launch_bounds__(BLOCK) void k_render(SceneHdr hdr, const double *__restrict__ tab,
+                                                  const int *__restrict__ itab, int W, int H, int depth, int rb,
+                                                  int shard, int nshards, int slab_rows, void *__restrict__ out,
+                                                  uint8_t *__restrict__ levels) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const Scene S{hdr, tab, itab};
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int x = blockIdx.x * TILE + (wave & 1) * 8 + (lane & 7);
+    const int ly = blockIdx.y * TILE + (wave >> 1) * 8 + (lane >> 3);
+    const bool inside = x < W && ly < slab_rows;
+    const int gy = ((ly / rb) * nshards + shard) * rb + (ly % rb);
+    const bool active = inside && gy < H;
+
+    // primary ray: ray_through_pixel/3 (:510-511) at {X/Width, Y/Height} (:112)
+    const double X = (double)x / (double)W, Y = (double)gy / (double)H;
+    const double px = 0.0 + ((X - 0.5) * hdr.screen_w + hdr.sx);
+    const double py = (Y - 0.5) * hdr.screen_h + hdr.sy;
+    const D3 cam = {hdr.cam_x, hdr.cam_y, hdr.cam_z};
+    const D3 d0 = normalize3(D3{px - hdr.cam_x, py - hdr.cam_y, hdr.dz});
+
+    D3 col = {0.0, 0.0, 0.0};
+    int nlev = 0;
+    if (ORDER == RT_ORDER_EXACT) {
+        double *st = reinterpret_cast<double *>(smem);               // [depth][BLOCK] distances
+        int *so = reinterpret_cast<int *>(smem + (size_t)depth * BLOCK * 8); // [depth][BLOCK] object ids
+        // forward: the reflection chain's nearest-object scans
+        D3 o = cam, d = d0;
+        bool alive = active;
+        for (int k = 0; k < depth; ++k) {
+            double t = 0;
+            int id = -1;
+            if (alive) id = (k == 0) ? nearest<true>(S, 0, o, d, t) : nearest<false>(S, 0, o, d, t);
+            if (id < 0) alive = false;
+            if (alive) {
+                st[k * BLOCK + tid] = t;
+                so[k * BLOCK + tid] = id;
+                nlev = k + 1;
+                if (k == depth - 1 || hdr.n_light == 0) alive = false;
+            }
+            if (alive) {
+                D3 hit, N;
+                hit_geom(S, id, o, d, t, hit, N);
+                d = bounce3(d, N);
+                o = hit;
+            }
+            if (__all(!alive)) break;
+        }
+        // backward: shade each level with the colour of the level below it (:216-247)
+        int maxlev = nlev;
+        for (int off = 32; off > 0; off >>= 1) maxlev = max(maxlev, __shfl_xor(maxlev, off));
+        for (int m = 0; m < maxlev; ++m) {
+            const int k = nlev - 1 - m;
+            const bool on = k >= 0;
+            D3 o2 = cam, d2 = d0, hit = cam, N = cam;
+            int id = 0;
+            if (on) {
+                for (int j = 0; j < k; ++j) { // replay the chain to level k
+                    hit_geom(S, so[j * BLOCK + tid], o2, d2, st[j * BLOCK + tid], hit, N);
+                    d2 = bounce3(d2, N);
+                    o2 = hit;
+                }
+                id = so[k * BLOCK + tid];
+                hit_geom(S, id, o2, d2, st[k * BLOCK + tid], hit, N);
+            }
+            const double refl = S.tab[hdr.o_obj + id * OBJ_W + 8];
+            const D3 R = {col.x * refl, col.y * refl, col.z * refl};
+            const D3 F = shade(S, id, d2, hit, N, R, on);
+            if (on) col = F;
+        }
+    } else {
+        // ORDER_FAST: colour = sum_k W_k * S_k with W_0 = 1, W_{k+1} = W_k * (L * refl_k)
+        D3 o = cam, d = d0;
+        double w = 1.0;
+        bool alive = active;
+        for (int k = 0; k < depth; ++k) {
+            double t = 0;
+            int id = -1;
+            if (alive) id = (k == 0) ? nearest<true>(S, 0, o, d, t) : nearest<false>(S, 0, o, d, t);
+            if (id < 0) alive = false;
+            D3 hit = cam, N = cam;
+            if (alive) {
+                nlev = k + 1;
+                hit_geom(S, id, o, d, t, hit, N);
+            }
+            if (__all(!alive)) break;
+            const D3 F = shade(S, alive ? id : 0, d, hit, N, D3{0.0, 0.0, 0.0}, alive);
+            if (alive) {
+                col.x = col.x + w * F.x;
+                col.y = col.y + w * F.y;
+                col.z = col.z + w * F.z;
+                w = w * (hdr.n_light_d * S.tab[hdr.o_obj + id * OBJ_W + 8]);
+                if (k == depth - 1 || hdr.n_light == 0) alive = false;
+                d = bounce3(d, N);
+                o = hit;
+            }
+        }
+    }
+    if (!inside) return;
+    const size_t pix = (size_t)ly * W + x;
+    if (PREC == RT_OUT_F64) {
+        double *o = reinterpret_cast<double *>(out) + pix * 3;
+        o[0] = col.x; o[1] = col.y; o[2] = col.z;
+    } else {
+        float *o = reinterpret_cast<float *>(out) + pix * 3;
+        o[0] = (float)col.x; o[1] = (float)col.y; o[2] = (float)col.z;
+    }
+    if (LEVELS) levels[pix] = (uint8_t)nlev;
+}
+
+} // namespace
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+struct rt_prepared {
+    int device;
+    SceneHdr hdr;
+    double *d_tab;
+    int *d_itab;
+};
+
+#define HIPCHK(x)                                                                                                  \
+    do {                                                                                                           \
+        hipError_t e_ = (x);                                                                                       \
+        if (e_ != hipSuccess) {                                                                                    \
+            std::fprintf(stderr, "rt_mi355x: %s failed: %s\n", #x, hipGetErrorString(e_));                        \
+            return RT_EHIP;                                                                                        \
+        }                                                                                                          \
+    } while (0)
+
+namespace {
+
+struct DevGuard { // restore the caller's current device on scope exit
+    int prev = -1;
+    explicit DevGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DevGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+template <int ORDER, int PREC>
+int launch_t(const rt_prepared *p, int W, int H, int depth, int rb, int shard, int nshards, int slab_rows, void *out,
+             uint8_t *levels, hipStream_t st) {
+    dim3 grid((W + TILE - 1) / TILE, (slab_rows + TILE - 1) / TILE);
+    size_t lds = ORDER == RT_ORDER_EXACT ? (size_t)depth * BLOCK * 12 : 0;
+    if (levels)
+        hipLaunchKernelGGL((k_render<ORDER, PREC, true>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
+                           H, depth, rb, shard, nshards, slab_rows, out, levels);
+    else
+        hipLaunchKernelGGL((k_render<ORDER, PREC, false>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
+                           H, depth, rb, shard, nshards, slab_rows, out, levels);
+    HIPCHK(hipGetLastError());
+    return RT_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char *rt_strerror(int code) {
+    switch (code) {
+    case RT_OK: return "ok";
+    case RT_DONE: return "done (width = height = 0)";
+    case RT_EBADARG: return "bad argument (malformed scene or sizes)";
+    case RT_ENODEV: return "no HIP device / device index out of range";
+    case RT_EHIP: return "HIP runtime error";
+    case RT_ENOMEM: return "out of memory";
+    case RT_ETOOBIG: return "size exceeds a library limit";
+    default: return "unknown error";
+    }
+}
+
+int rt_device_count(int *count) {
+    if (!count) return RT_EBADARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return n > 0 ? RT_OK : RT_ENODEV;
+}
+
+int rt_scene_check(const rt_elem *scene, uint32_t n) { return check_scene(scene, n); }
+
+int rt_scene_canon(rt_elem *scene, uint32_t n) { return fill_canon(scene, n); }
+
+uint32_t rt_shard_rows(uint32_t height, uint32_t row_block, uint32_t nshards) {
+    if (row_block == 0 || nshards == 0) return 0;
+    uint64_t span = (uint64_t)row_block * nshards;
+    uint64_t blocks = (height + span - 1) / span;
+    return (uint32_t)(blocks * row_block);
+}
+
+int rt_prepare(const rt_elem *scene, uint32_t n, int device, rt_prepared **out) {
+    if (!out) return RT_EBADARG;
+    *out = nullptr;
+    Compiled c;
+    int rc = compile_scene(scene, n, c);
+    if (rc != RT_OK) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return RT_ENODEV;
+    DevGuard g(device);
+    rt_prepared *p = new (std::nothrow) rt_prepared();
+    if (!p) return RT_ENOMEM;
+    p->device = device;
+    p->hdr = c.hdr;
+    if (hipMalloc(&p->d_tab, c.tab.size() * sizeof(double)) != hipSuccess) {
+        delete p;
+        return RT_ENOMEM;
+    }
+    if (hipMalloc(&p->d_itab, c.itab.size() * sizeof(int)) != hipSuccess) {
+        (void)hipFree(p->d_tab);
+        delete p;
+        return RT_ENOMEM;
+    }
+    if (hipMemcpy(p->d_tab, c.tab.data(), c.tab.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_itab, c.itab.data(), c.itab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(p->d_tab);
+        (void)hipFree(p->d_itab);
+        delete p;
+        return RT_EHIP;
+    }
+    *out = p;
+    return RT_OK;
+}
+
+int rt_release(rt_prepared *p) {
+    if (!p) return RT_EBADARG;
+    DevGuard g(p->device);
+    (void)hipFree(p->d_tab);
+    (void)hipFree(p->d_itab);
+    delete p;
+    return RT_OK;
+}
+
+int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, uint32_t row_block, uint32_t shard,
+              uint32_t nshards, int precision, int order, void *d_out, uint8_t *d_levels, void *stream) {
+    if (!p || !d_out) return RT_EBADARG;
+    if (width == 0 && height == 0) return RT_DONE;
+    if (width == 0 || height == 0) return RT_EBADARG;
+    if (depth > RT_MAX_DEPTH) return RT_ETOOBIG;
+    if (row_block == 0 || nshards == 0 || shard >= nshards) return RT_EBADARG;
+    if (precision != RT_OUT_F64 && precision != RT_OUT_F32) return RT_EBADARG;
+    if (order != RT_ORDER_EXACT && order != RT_ORDER_FAST) return RT_EBADARG;
+    if (width > (1u << 20) || height > (1u << 20)) return RT_ETOOBIG;
+    uint32_t slab = rt_shard_rows(height, row_block, nshards);
+    if ((uint64_t)slab > 65535ull * TILE) return RT_ETOOBIG;
+    DevGuard g(p->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int W = (int)width, H = (int)height, D = (int)depth, rb = (int)row_block, sh = (int)shard, ns = (int)nshards;
+    if (order == RT_ORDER_EXACT)
+        return precision == RT_OUT_F64
+                   ? launch_t<RT_ORDER_EXACT, RT_OUT_F64>(p, W, H, D, rb, sh, ns, (int)slab, d_out, d_levels, st)
+                   : launch_t<RT_ORDER_EXACT, RT_OUT_F32>(p, W, H, D, rb, sh, ns, (int)slab, d_out, d_levels, st);
+    return precision == RT_OUT_F64
+               ? launch_t<RT_ORDER_FAST, RT_OUT_F64>(p, W, H, D, rb, sh, ns, (int)slab, d_out, d_levels, st)
+               : launch_t<RT_ORDER_FAST, RT_OUT_F32>(p, W, H, D, rb, sh, ns, (int)slab, d_out, d_levels, st);
+}
+
+// Copy the blocks of one shard's slab to their rows in a row-major image.  dst_kind selects
+// hipMemcpyDeviceToDevice or DeviceToHost.
+static int scatter_slab(const char *slab, uint32_t rowbytes, uint32_t H, uint32_t rb, uint32_t shard,
+                        uint32_t nshards, char *image, hipMemcpyKind kind, hipStream_t st) {
+    uint64_t blk_bytes = (uint64_t)rb * rowbytes;
+    uint32_t nfull = 0;
+    while ((((uint64_t)nfull * nshards + shard) * rb + rb) <= H) nfull++;
+    if (nfull)
+        HIPCHK(hipMemcpy2DAsync(image + (uint64_t)shard * blk_bytes, (size_t)blk_bytes * nshards, slab,
+                                (size_t)blk_bytes, (size_t)blk_bytes, nfull, kind, st));
+    uint64_t g0 = ((uint64_t)nfull * nshards + shard) * rb;
+    if (g0 < H) { // one partial block at the bottom of the image
+        uint64_t rows = H - g0;
+        HIPCHK(hipMemcpyAsync(image + g0 * rowbytes, slab + (uint64_t)nfull * blk_bytes, rows * rowbytes, kind, st));
+    }
+    return RT_OK;
+}
+
+int rt_unshard(const void *d_slabs, uint32_t width, uint32_t height, uint32_t row_block, uint32_t nshards,
+               int precision, void *d_image, void *stream) {
+    if (!d_slabs || !d_image || width == 0 || height == 0 || row_block == 0 || nshards == 0) return RT_EBADARG;
+    if (precision != RT_OUT_F64 && precision != RT_OUT_F32) return RT_EBADARG;
+    uint32_t rowbytes = width * 3 * (precision == RT_OUT_F64 ? 8 : 4);
+    uint64_t slab_bytes = (uint64_t)rt_shard_rows(height, row_block, nshards) * rowbytes;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    for (uint32_t s = 0; s < nshards; s++) {
+        int rc = scatter_slab(static_cast<const char *>(d_slabs) + s * slab_bytes, rowbytes, height, row_block, s,
+                              nshards, static_cast<char *>(d_image), hipMemcpyDeviceToDevice, st);
+        if (rc != RT_OK) return rc;
+    }
+    return RT_OK;
+}
+
+int rt_render(const rt_elem *scene, uint32_t n, uint32_t width, uint32_t height, uint32_t depth,
+              const rt_opts *opts, void *out_rgb, rt_stats *stats) {
+    auto t_begin = std::chrono::steady_clock::now();
+    if (width == 0 && height == 0) return RT_DONE;
+    if (width == 0 || height == 0) return RT_EBADARG;
+    if (!out_rgb) return RT_EBADARG;
+    if (depth > RT_MAX_DEPTH) return RT_ETOOBIG;
+    rt_opts o;
+    std::memset(&o, 0, sizeof(o));
+    o.ndev = 1;
+    o.row_block = 16;
+    if (opts && opts->struct_size) {
+        std::memcpy(&o, opts, opts->struct_size < sizeof(o) ? opts->struct_size : sizeof(o));
+        if (o.row_block == 0) o.row_block = 16;
+        if (o.ndev == 0) o.ndev = 1;
+    }
+    int rc = check_scene(scene, n);
+    if (rc != RT_OK) return rc;
+    int navail = 0;
+    if (hipGetDeviceCount(&navail) != hipSuccess || navail <= 0) return RT_ENODEV;
+    if (o.ndev < 0) o.ndev = navail - o.first_dev;
+    if (o.first_dev < 0 || o.ndev <= 0 || o.first_dev + o.ndev > navail) return RT_ENODEV;
+    const uint32_t ns = (uint32_t)o.ndev, rb = o.row_block;
+    const uint32_t slab = rt_shard_rows(height, rb, ns);
+    const size_t esz = o.precision == RT_OUT_F32 ? 4 : 8;
+    const uint32_t rowbytes = width * 3 * (uint32_t)esz;
+
+    struct Dev {
+        rt_prepared *p = nullptr;
+        void *d_out = nullptr;
+        uint8_t *d_lv = nullptr;
+        hipStream_t st = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+    };
+    std::vector<Dev> devs(ns);
+    int err = RT_OK;
+    for (uint32_t s = 0; s < ns && err == RT_OK; s++) {
+        Dev &dv = devs[s];
+        int dev = o.first_dev + (int)s;
+        err = rt_prepare(scene, n, dev, &dv.p);
+        if (err != RT_OK) break;
+        DevGuard g(dev);
+        if (hipStreamCreateWithFlags(&dv.st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreate(&dv.e0) != hipSuccess || hipEventCreate(&dv.e1) != hipSuccess) {
+            err = RT_EHIP;
+            break;
+        }
+        if (hipMalloc(&dv.d_out, (size_t)slab * rowbytes) != hipSuccess ||
+            (o.out_levels && hipMalloc((void **)&dv.d_lv, (size_t)slab * width) != hipSuccess)) {
+            err = RT_ENOMEM;
+            break;
+        }
+        (void)hipEventRecord(dv.e0, dv.st);
+        err = rt_launch(dv.p, width, height, depth, rb, s, ns, o.precision, o.order, dv.d_out, dv.d_lv, dv.st);
+        if (err != RT_OK) break;
+        (void)hipEventRecord(dv.e1, dv.st);
+        err = scatter_slab(static_cast<const char *>(dv.d_out), rowbytes, height, rb, s, ns,
+                           static_cast<char *>(out_rgb), hipMemcpyDeviceToHost, dv.st);
+        if (err == RT_OK && o.out_levels)
+            err = scatter_slab(reinterpret_cast<const char *>(dv.d_lv), width, height, rb, s, ns,
+                               reinterpret_cast<char *>(o.out_levels), hipMemcpyDeviceToHost, dv.st);
+    }
+    double kms = 0;
+    for (uint32_t s = 0; s < ns; s++) {
+        Dev &dv = devs[s];
+        if (!dv.p) continue;
+        DevGuard g(dv.p->device);
+        if (dv.st) {
+            if (hipStreamSynchronize(dv.st) != hipSuccess && err == RT_OK) err = RT_EHIP;
+            float ms = 0;
+            if (err == RT_OK && hipEventElapsedTime(&ms, dv.e0, dv.e1) == hipSuccess && ms > kms) kms = ms;
+        }
+        if (dv.e0) (void)hipEventDestroy(dv.e0);
+        if (dv.e1) (void)hipEventDestroy(dv.e1);
+        if (dv.st) (void)hipStreamDestroy(dv.st);
+        if (dv.d_out) (void)hipFree(dv.d_out);
+        if (dv.d_lv) (void)hipFree(dv.d_lv);
+        rt_release(dv.p);
+    }
+    if (stats) {
+        stats->kernel_ms = kms;
+        stats->total_ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count();
+        stats->pixels = (uint64_t)width * height;
+        stats->ndev = (int32_t)ns;
+        stats->reserved = 0;
+    }
+    return err;
+}
+
+} // extern "C"

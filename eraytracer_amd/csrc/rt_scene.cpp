@@ -1,0 +1,262 @@
+// rt_scene.cpp — host-side scene compiler: validates an rt_elem list (the marshalled
+// reference scene, raytracer.erl:618-665) and lays it out for the kernel (rt_layout.h).
+//
+// Every precomputed quantity is produced with the reference's operation order, in IEEE
+// binary64, compiled with -ffp-contract=off, so the kernel sees bit-identical values to
+// those the reference computes per ray.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/rt_mi355x.h"
+#include "rt_layout.h"
+#include "rt_scene.h"
+
+namespace rtl {
+
+static bool finite3(const rt_vec3 &v) { return std::isfinite(v.x) && std::isfinite(v.y) && std::isfinite(v.z); }
+static bool finite_mat(const rt_material &m) {
+    return finite3(m.colour) && std::isfinite(m.specular_power) && std::isfinite(m.shininess) &&
+           std::isfinite(m.reflectivity);
+}
+
+static bool elem_ok(const rt_elem &e) {
+    switch (e.kind) {
+    case RT_CAMERA:
+        return finite3(e.u.camera.location) && finite3(e.u.camera.rotation) && std::isfinite(e.u.camera.fov) &&
+               std::isfinite(e.u.camera.screen_width) && std::isfinite(e.u.camera.screen_height);
+    case RT_POINT_LIGHT:
+        return finite3(e.u.point_light.diffuse_colour) && finite3(e.u.point_light.location) &&
+               finite3(e.u.point_light.specular_colour);
+    case RT_SPHERE:
+        return std::isfinite(e.u.sphere.radius) && finite3(e.u.sphere.center) && finite_mat(e.u.sphere.material);
+    case RT_TRIANGLE:
+        return finite3(e.u.triangle.v1) && finite3(e.u.triangle.v2) && finite3(e.u.triangle.v3) &&
+               finite_mat(e.u.triangle.material);
+    case RT_PLANE:
+        return finite3(e.u.plane.normal) && std::isfinite(e.u.plane.distance) && finite_mat(e.u.plane.material);
+    case RT_OTHER:
+        return true;
+    default:
+        return false;
+    }
+}
+
+static size_t payload_bytes(int kind) {
+    switch (kind) {
+    case RT_CAMERA: return sizeof(((rt_elem *)0)->u.camera);
+    case RT_POINT_LIGHT: return sizeof(((rt_elem *)0)->u.point_light);
+    case RT_SPHERE: return sizeof(((rt_elem *)0)->u.sphere);
+    case RT_TRIANGLE: return sizeof(((rt_elem *)0)->u.triangle);
+    case RT_PLANE: return sizeof(((rt_elem *)0)->u.plane);
+    default: return 0;
+    }
+}
+
+int check_scene(const rt_elem *e, uint32_t n) {
+    if (!e || n < 1) return RT_EBADARG;         // [Camera|Rest] must match (raytracer.erl:180)
+    if (e[0].kind != RT_CAMERA) return RT_EBADARG; // Camera#camera.location would crash (:488)
+    uint32_t nobj = 0, nl = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (!elem_ok(e[i])) return RT_EBADARG;
+        if (e[i].canon < -1 || e[i].canon > (int32_t)i) return RT_EBADARG;
+        if (e[i].canon >= 0 && e[e[i].canon].kind != e[i].kind) return RT_EBADARG;
+        if (i == 0) continue;
+        if (e[i].kind == RT_SPHERE || e[i].kind == RT_TRIANGLE || e[i].kind == RT_PLANE) nobj++;
+        if (e[i].kind == RT_POINT_LIGHT) nl++;
+    }
+    if (nobj > RT_MAX_OBJECTS || nl > RT_MAX_LIGHTS) return RT_ETOOBIG;
+    return RT_OK;
+}
+
+int fill_canon(rt_elem *e, uint32_t n) {
+    if (!e) return RT_EBADARG;
+    for (uint32_t i = 0; i < n; i++) {
+        if (e[i].canon >= 0) continue;
+        e[i].canon = (int32_t)i;
+        size_t nb = payload_bytes(e[i].kind);
+        for (uint32_t j = 0; j < i; j++) {
+            if (e[j].kind == e[i].kind && (int32_t)j == e[j].canon && nb &&
+                std::memcmp(&e[j].u, &e[i].u, nb) == 0) {
+                e[i].canon = (int32_t)j;
+                break;
+            }
+        }
+    }
+    return RT_OK;
+}
+
+// resolve canon chains to the first element of each equality class
+static int root(const std::vector<rt_elem> &e, int i) {
+    while (e[i].canon >= 0 && e[i].canon != i) i = e[i].canon;
+    return i;
+}
+
+int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
+    int rc = check_scene(in, n);
+    if (rc != RT_OK) return rc;
+    std::vector<rt_elem> e(in, in + n);
+    fill_canon(e.data(), n);
+
+    const rt_elem &cam = e[0];
+    std::vector<int> compact(n, -1);
+    std::vector<int> objs, lights;
+    for (uint32_t i = 1; i < n; i++) {
+        int k = e[i].kind;
+        if (k == RT_SPHERE || k == RT_TRIANGLE || k == RT_PLANE) {
+            compact[i] = (int)objs.size();
+            objs.push_back((int)i);
+        } else if (k == RT_POINT_LIGHT) {
+            lights.push_back((int)i);
+        }
+    }
+    std::vector<int> sph, tri, pl;
+    for (int i : objs) {
+        if (e[i].kind == RT_SPHERE) sph.push_back(i);
+        else if (e[i].kind == RT_TRIANGLE) tri.push_back(i);
+        else pl.push_back(i);
+    }
+
+    SceneHdr &h = out.hdr;
+    std::memset(&h, 0, sizeof(h));
+    h.n_sph = (int)sph.size();
+    h.n_tri = (int)tri.size();
+    h.n_pl = (int)pl.size();
+    h.n_obj = (int)objs.size();
+    h.n_light = (int)lights.size();
+    h.n_org = 1 + h.n_light;
+
+    // origins: slot 0 = camera location, slot 1+i = light i location
+    std::vector<rt_vec3> org;
+    org.push_back(cam.u.camera.location);
+    for (int li : lights) org.push_back(e[li].u.point_light.location);
+
+    std::vector<double> &t = out.tab;
+    std::vector<int> &it = out.itab;
+    t.clear();
+    it.clear();
+
+    // spheres (ray_sphere_intersect/2, :364-397)
+    h.o_sph = (int)t.size();
+    for (int i : sph) {
+        const auto &s = e[i].u.sphere;
+        double r = s.radius;
+        t.insert(t.end(), {s.center.x, s.center.y, s.center.z, r * r});
+    }
+    h.o_sph_org = (int)t.size();
+    for (const rt_vec3 &o : org) {
+        for (int i : sph) {
+            const auto &s = e[i].u.sphere;
+            double X0 = o.x, Y0 = o.y, Z0 = o.z, Xc = s.center.x, Yc = s.center.y, Zc = s.center.z;
+            double r = s.radius;
+            double C = (X0 - Xc) * (X0 - Xc) + (Y0 - Yc) * (Y0 - Yc) + (Z0 - Zc) * (Z0 - Zc) - r * r;
+            t.insert(t.end(), {X0 - Xc, Y0 - Yc, Z0 - Zc, C});
+        }
+    }
+    // triangles (ray_triangle_intersect/2, :402-455)
+    h.o_tri = (int)t.size();
+    for (int i : tri) {
+        const auto &tr = e[i].u.triangle;
+        double e1x = tr.v2.x - tr.v1.x, e1y = tr.v2.y - tr.v1.y, e1z = tr.v2.z - tr.v1.z;
+        double e2x = tr.v3.x - tr.v1.x, e2y = tr.v3.y - tr.v1.y, e2z = tr.v3.z - tr.v1.z;
+        t.insert(t.end(), {tr.v1.x, tr.v1.y, tr.v1.z, e1x, e1y, e1z, e2x, e2y, e2z, 0, 0, 0});
+    }
+    h.o_tri_org = (int)t.size();
+    for (const rt_vec3 &o : org) {
+        for (int i : tri) {
+            const auto &tr = e[i].u.triangle;
+            double e1x = tr.v2.x - tr.v1.x, e1y = tr.v2.y - tr.v1.y, e1z = tr.v2.z - tr.v1.z;
+            double Tx = o.x - tr.v1.x, Ty = o.y - tr.v1.y, Tz = o.z - tr.v1.z;
+            // Q = vector_cross_product(T, Edge1) (:431, :549-552)
+            double Qx = Ty * e1z - Tz * e1y, Qy = Tz * e1x - Tx * e1z, Qz = Tx * e1y - Ty * e1x;
+            t.insert(t.end(), {Tx, Ty, Tz, Qx, Qy, Qz, 0, 0});
+        }
+    }
+    // planes (ray_plane_intersect/2, :461-480)
+    h.o_pl = (int)t.size();
+    for (int i : pl) {
+        const auto &p = e[i].u.plane;
+        t.insert(t.end(), {p.normal.x, p.normal.y, p.normal.z, p.distance});
+    }
+    h.o_pl_org = (int)t.size();
+    for (const rt_vec3 &o : org) {
+        for (int i : pl) {
+            const auto &p = e[i].u.plane;
+            double V0 = -(p.normal.x * o.x + p.normal.y * o.y + p.normal.z * o.z + p.distance);
+            t.push_back(V0);
+        }
+    }
+    // per-object shading records, by compact id
+    h.o_obj = (int)t.size();
+    for (int i : objs) {
+        const rt_elem &o = e[i];
+        const rt_material *m;
+        double a = 0, b = 0, c = 0;
+        if (o.kind == RT_SPHERE) {
+            m = &o.u.sphere.material;
+            a = o.u.sphere.center.x; b = o.u.sphere.center.y; c = o.u.sphere.center.z;
+        } else if (o.kind == RT_TRIANGLE) {
+            m = &o.u.triangle.material;
+            // Normal = vector_normalize(vector_cross_product(v1, v2)) (:448-451), a constant
+            const rt_vec3 &v1 = o.u.triangle.v1, &v2 = o.u.triangle.v2;
+            double nx = v1.y * v2.z - v1.z * v2.y, ny = v1.z * v2.x - v1.x * v2.z, nz = v1.x * v2.y - v1.y * v2.x;
+            double mag = std::sqrt(nx * nx + ny * ny + nz * nz);
+            if (mag == 0) {
+                a = b = c = 0;
+            } else {
+                double s = 1 / std::sqrt(nx * nx + ny * ny + nz * nz);
+                a = nx * s; b = ny * s; c = nz * s;
+            }
+        } else {
+            m = &o.u.plane.material;
+            a = o.u.plane.normal.x; b = o.u.plane.normal.y; c = o.u.plane.normal.z;
+        }
+        t.insert(t.end(), {a, b, c, m->colour.x, m->colour.y, m->colour.z, m->specular_power, m->shininess,
+                           m->reflectivity, 0, 0, 0});
+    }
+    h.o_light = (int)t.size();
+    for (int li : lights) {
+        const auto &L = e[li].u.point_light;
+        t.insert(t.end(), {L.diffuse_colour.x, L.diffuse_colour.y, L.diffuse_colour.z, L.location.x, L.location.y,
+                           L.location.z, L.specular_colour.x, L.specular_colour.y, L.specular_colour.z, 0, 0, 0});
+    }
+    if (t.empty()) t.push_back(0);
+
+    // int table
+    h.i_sph_id = (int)it.size();
+    for (int i : sph) it.push_back(compact[i]);
+    h.i_tri_id = (int)it.size();
+    for (int i : tri) it.push_back(compact[i]);
+    h.i_pl_id = (int)it.size();
+    for (int i : pl) it.push_back(compact[i]);
+    h.i_obj_meta = (int)it.size();
+    for (int i : objs) {
+        int kind = e[i].kind == RT_SPHERE ? K_SPHERE : (e[i].kind == RT_TRIANGLE ? K_TRIANGLE : K_PLANE);
+        int local = 0;
+        const std::vector<int> &grp = kind == K_SPHERE ? sph : (kind == K_TRIANGLE ? tri : pl);
+        for (size_t q = 0; q < grp.size(); q++)
+            if (grp[q] == i) local = (int)q;
+        it.insert(it.end(), {kind, local, compact[root(e, i)], 0});
+    }
+    if (it.empty()) it.push_back(0);
+
+    // camera: point_on_screen/3 (:486-503) with focal_length/2 (:483-484).
+    // Sum = foldl(fun(V, S) -> vector_add(V, S) end, Location, [ {0*F,0*F,1*F}, {(X-0.5)*SW,0,0},
+    // {0,(Y-0.5)*SH,0} ]); the pixel-invariant parts are folded here in the same order.
+    double SW = cam.u.camera.screen_width, SH = cam.u.camera.screen_height;
+    double F = SW / (2 * std::tan(cam.u.camera.fov * (M_PI / 180) / 2));
+    const rt_vec3 &L = cam.u.camera.location;
+    h.cam_x = L.x; h.cam_y = L.y; h.cam_z = L.z;
+    h.sx = 0 * F + L.x;                       // x after step 1; step 2 adds (X-0.5)*SW, step 3 adds 0
+    h.sy = 0.0 + (0 * F + L.y);               // y after steps 1-2; step 3 adds (Y-0.5)*SH
+    double pz = 0.0 + (0.0 + (1 * F + L.z));  // z after steps 1-3
+    h.dz = pz - L.z;                          // vector_sub(Through, From).z (:507)
+    if (!std::isfinite(F) || !std::isfinite(h.sx) || !std::isfinite(h.sy) || !std::isfinite(h.dz))
+        return RT_EBADARG; // Erlang raises badarith where binary64 would overflow
+    h.screen_w = SW;
+    h.screen_h = SH;
+    h.n_light_d = (double)h.n_light;
+    return RT_OK;
+}
+
+} // namespace rtl

@@ -1,0 +1,164 @@
+/*
+ * rt_mi355x.h — C-ABI boundary of the MI355X-native per-pixel render path.
+ *
+ * This library replaces the pixel loop of the reference ray tracer
+ * (plouj/eraytracer, raytracer.erl).  The reference's strategy interface is
+ *
+ *     F(Width, Height, Scene, Recursion_depth) -> done | [{Key, {R,G,B}}]
+ *
+ * implemented by raytraced_pixel_list_simple/4      (raytracer.erl:86-99),
+ *                raytraced_pixel_list_concurrent/4  (raytracer.erl:101-119),
+ *                raytraced_pixel_list_distributed/4 (raytracer.erl:121-149),
+ * chosen by tracing_function/1 (raytracer.erl:714-719) and called once by
+ * raytrace/5 (raytracer.erl:723-733).  Every pixel runs
+ * trace_ray_through_pixel/3 (raytracer.erl:180-184) and the shading /
+ * intersection functions below it (raytracer.erl:186-511).
+ *
+ * The host (an erl_nif shim, a ctypes binding, a C++ program) marshals the
+ * scene list (raytracer.erl:618-665 for the default one) into an array of
+ * rt_elem records in LIST ORDER, element 0 being the camera, and calls
+ * rt_render().  The result is the W*H*3 framebuffer in row-major order, i.e.
+ * exactly the {R,G,B} values of the reference's list, in the list's order.
+ * The keys are implied: simple uses key 1 for every pixel (raytracer.erl:95),
+ * concurrent/distributed use X+Y*Width (raytracer.erl:112,173) and sort by it.
+ *
+ * All arithmetic is IEEE binary64 in the reference's operation order
+ * (Erlang floats are doubles).  No pointer passed in is retained after a call
+ * returns.  Every entry point returns 0 (RT_OK), RT_DONE, or a negative RT_E*
+ * code; rt_strerror() names it.
+ */
+#ifndef RT_MI355X_H
+#define RT_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- return codes ------------------------------------------------------- */
+#define RT_OK 0
+#define RT_DONE 1          /* W = H = 0: the reference returns the atom `done` (raytracer.erl:86,101,121) */
+#define RT_EBADARG (-1)    /* malformed scene / sizes: the reference crashes (function_clause, badrecord) */
+#define RT_ENODEV (-2)     /* no HIP device, or device index out of range */
+#define RT_EHIP (-3)       /* a HIP runtime call failed */
+#define RT_ENOMEM (-4)     /* host or device allocation failed */
+#define RT_ETOOBIG (-5)    /* size exceeds a documented limit (see RT_MAX_*) */
+
+#define RT_MAX_DEPTH 16    /* recursion depths above this are rejected */
+#define RT_MAX_OBJECTS 4096
+#define RT_MAX_LIGHTS 64
+
+/* ---- scene records, mirroring the reference's records (raytracer.erl:72-81) -- */
+enum rt_kind {
+    RT_CAMERA = 0,      /* #camera{location, rotation, fov, screen}             :76 */
+    RT_POINT_LIGHT = 1, /* #point_light{diffuse_colour, location, specular_colour} :81 */
+    RT_SPHERE = 2,      /* #sphere{radius, center, material}                    :78 */
+    RT_TRIANGLE = 3,    /* #triangle{v1, v2, v3, material}                      :79 */
+    RT_PLANE = 4,       /* #plane{normal, distance, material}                   :80 */
+    RT_OTHER = 5        /* any other term: ray_object_intersect/2 -> none (:357),
+                           lighting_function skips it (:248) */
+};
+
+typedef struct rt_vec3 {
+    double x, y, z; /* #vector{x, y, z} / #colour{r, g, b} (:72-73) */
+} rt_vec3;
+
+typedef struct rt_material { /* #material{colour, specular_power, shininess, reflectivity} (:77) */
+    rt_vec3 colour;
+    double specular_power;
+    double shininess;
+    double reflectivity;
+} rt_material;
+
+typedef struct rt_elem {
+    int32_t kind;  /* enum rt_kind */
+    /* canon: index (into this array) of the FIRST element that is exactly equal
+     * (=:=, so 4 and 4.0 differ) to this one; shadow_factor/4 (raytracer.erl:
+     * 256-267) lights a hit iff the nearest object seen from the light MATCHES
+     * the hit object term, so duplicates count as the same object.  Pass -1 to
+     * let the library decide by bitwise equality of kind and every field. */
+    int32_t canon;
+    union {
+        struct { rt_vec3 location, rotation; double fov, screen_width, screen_height; } camera;
+        struct { rt_vec3 diffuse_colour, location, specular_colour; } point_light;
+        struct { double radius; rt_vec3 center; rt_material material; } sphere;
+        struct { rt_vec3 v1, v2, v3; rt_material material; } triangle;
+        struct { rt_vec3 normal; double distance; rt_material material; } plane;
+        double raw[12];
+    } u;
+} rt_elem;
+
+/* ---- options / statistics ---------------------------------------------------- */
+#define RT_OUT_F64 0   /* out_rgb is double[H][W][3] (the reference's values, exact) */
+#define RT_OUT_F32 1   /* out_rgb is float[H][W][3]  (the "float3 framebuffer") */
+
+#define RT_ORDER_EXACT 0 /* reflection added once per light, reference fold order (bit-identical colour sums) */
+#define RT_ORDER_FAST 1  /* forward-only reassociated accumulation (|delta| ~ 1e-15, same hit decisions) */
+
+typedef struct rt_opts {
+    uint32_t struct_size; /* sizeof(rt_opts); 0 or a NULL opts pointer selects every default */
+    int32_t first_dev;    /* first HIP device (default 0) */
+    int32_t ndev;         /* devices used by rt_render in this process (default 1; -1 = all visible) */
+    int32_t precision;    /* RT_OUT_F64 (default) or RT_OUT_F32 */
+    int32_t order;        /* RT_ORDER_EXACT (default) or RT_ORDER_FAST */
+    uint32_t row_block;   /* multi-device interleave granularity in rows (default 16) */
+    uint8_t *out_levels;  /* optional host W*H bytes: reflection-chain levels that hit, per pixel */
+} rt_opts;
+
+typedef struct rt_stats {
+    double kernel_ms;   /* device time of the render kernels (max over devices) */
+    double total_ms;    /* wall time of the whole call, boundary to boundary */
+    uint64_t pixels;    /* W*H */
+    int32_t ndev;       /* devices actually used */
+    int32_t reserved;
+} rt_stats;
+
+/* ---- library / device ------------------------------------------------------------ */
+int rt_abi_version(void);
+const char *rt_strerror(int code);
+int rt_device_count(int *count);
+
+/* Validate a scene list without rendering (0 = a scene the reference would
+ * trace without crashing for a pixel that hits any object). */
+int rt_scene_check(const rt_elem *scene, uint32_t n_elems);
+
+/* Fill canon[] for elems whose canon is -1 (bitwise-equality rule). */
+int rt_scene_canon(rt_elem *scene, uint32_t n_elems);
+
+/* ---- one-shot render: the drop-in for raytraced_pixel_list_{simple,concurrent,distributed} --
+ * Replaces the whole pixel loop (raytracer.erl:86-178): for every pixel (x,y),
+ * row-major, out = trace_ray_through_pixel({x/W, y/H}, Scene, Depth).
+ * out_rgb: caller-owned host memory, W*H*3 elements of the chosen precision.
+ * Returns RT_DONE for W = H = 0, RT_EBADARG if exactly one of them is 0. */
+int rt_render(const rt_elem *scene, uint32_t n_elems, uint32_t width, uint32_t height,
+              uint32_t depth, const rt_opts *opts, void *out_rgb, rt_stats *stats);
+
+/* ---- resident-scene API (device buffers, caller's HIP stream) -------------------
+ * rt_prepare uploads the scene (and its per-origin constant tables) to one device.
+ * rt_launch renders shard `shard` of `nshards` into device memory, asynchronously
+ * on `stream` (a hipStream_t; NULL = the null stream).  Rows are dealt to shards
+ * in interleaved blocks of `row_block` rows: global row g belongs to shard
+ * (g / row_block) % nshards.  d_out receives the shard's rows packed in order,
+ * rt_shard_rows(height,row_block,nshards) rows of width*3 elements; slab rows past
+ * the image are written as zero.  d_levels (optional) gets one byte per slab pixel. */
+typedef struct rt_prepared rt_prepared;
+
+int rt_prepare(const rt_elem *scene, uint32_t n_elems, int device, rt_prepared **out);
+uint32_t rt_shard_rows(uint32_t height, uint32_t row_block, uint32_t nshards);
+int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth,
+              uint32_t row_block, uint32_t shard, uint32_t nshards, int precision, int order,
+              void *d_out, uint8_t *d_levels, void *stream);
+/* Reassemble nshards gathered slabs (d_slabs = [nshards][shard_rows][W*3]) into the
+ * row-major image d_image ([H][W*3]), on `stream`. */
+int rt_unshard(const void *d_slabs, uint32_t width, uint32_t height, uint32_t row_block,
+               uint32_t nshards, int precision, void *d_image, void *stream);
+int rt_release(rt_prepared *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_MI355X_H */
