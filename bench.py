@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X render path (BASELINE.json metric: Mpixels/s at 4096x4096,
+recursion depth 5, on 1/2/4/8 MI355X).
+
+One step = one frame of the workload (default: synthetic scene S64 — 64 spheres, 4 point
+lights — at 4096x4096, depth 5, BASELINE.json configs[2]) rendered by the HIP kernel
+into HBM; with N ranks the frame's rows are split over the ranks (strong scaling) and
+gathered to rank 0 over RCCL, then put back in row order.  Inputs (the compiled scene)
+are resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scene s64] [--size 4096] [--depth 5]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  Extra keys: "roofline" (the binding FP64-VALU roofline of
+the render kernel), "roofline_hbm" (the memory roofline the north star asks for),
+"cpu_baseline" (the C oracle running the reference's literal recursion on the host's
+cores over a bounded sample of the same frame — the BEAM is not installed on the box),
+"kernel_mpx_s" and "boundary_mpx_s" (host-buffer rt_render, PCIe included).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP64_VALU_TOPS = 39.3   # MI355X FP64 vector 78.6 TFLOP/s counting an FMA as 2 (spec); this path has no FMA
+PEAK_HBM_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scene", default="s64")
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--order", default="exact", choices=["exact", "fast"])
+    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--row-block", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-boundary", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, W, H, depth, target_s):
+    """The C oracle in the reference's literal recursion (lighting_function recomputes the
+    reflection per light, raytracer.erl:211-224), threaded over the box's CPU share, on a
+    bounded sample of rows spread over the same frame."""
+    from eraytracer_amd import _native as N
+    from oracle import oracle as O
+    O.build()
+    el = N.marshal(scene)
+    threads = min(16, os.cpu_count() or 1)
+    # calibrate on one row, then take evenly spaced rows to fill ~target_s seconds
+    t0 = time.perf_counter()
+    O.render(el, W, H, depth, mode=O.LITERAL, threads=threads, row0=H // 2, nrows=1)
+    per_row = max(time.perf_counter() - t0, 1e-4)
+    nrows = int(max(1, min(H, target_s / per_row)))
+    rows = sorted(set(int(r) for r in [(i * H) // nrows + (H // nrows) // 2 for i in range(nrows)]))
+    t0 = time.perf_counter()
+    for r in rows:
+        O.render(el, W, H, depth, mode=O.LITERAL, threads=threads, row0=r, nrows=1)
+    dt = time.perf_counter() - t0
+    px = len(rows) * W
+    return {"value": px / dt / 1e6, "unit": "Mpixels/s", "cores": threads, "kind": "port",
+            "sample": f"{len(rows)} evenly spaced rows x {W} px of the same {W}x{H} depth-{depth} frame "
+                      f"({px} px, {dt:.1f} s), oracle/rt_oracle.c ORC_LITERAL (the reference's per-light "
+                      f"reflection recursion), {threads} threads; BEAM (erl) is not installed on the box"}
+
+
+def traffic_from_profiles(workload_key):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary of the same workload
+    (profiles/*pmc*.json written by scripts/profile.sh), or None."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("workload") == workload_key and d.get("hbm_bytes_per_launch") is not None:
+            best = (d["hbm_bytes_per_launch"], os.path.relpath(p, ROOT))
+    return best
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from eraytracer_amd import scenes, workload
+    from eraytracer_amd.dist import FrameRenderer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("bench.py: --gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    W = H = args.size
+    scene = scenes.named(args.scene)
+    counts = workload.scene_counts(scene)
+    fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
+                       precision=args.precision, order=args.order)
+
+    # untimed: work count of this rank's rows (levels of every pixel's reflection chain)
+    lv_fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
+                          precision=args.precision, order=args.order, levels=True)
+    lv_fr.launch()
+    torch.cuda.synchronize()
+    from eraytracer_amd.dist import shard_global_rows
+    valid = torch.from_numpy(shard_global_rows(H, args.row_block, world, rank) >= 0).to(lv_fr.levels.device)
+    hist = torch.bincount(lv_fr.levels[valid].flatten().to(torch.int64), minlength=args.depth + 1).cpu().numpy()
+    lv_fr.close()
+    del lv_fr
+    ops_rank = workload.ops_from_levels(hist, args.depth, counts)
+    px_rank = int(hist.sum())
+
+    for _ in range(args.warmup):
+        fr.step()
+    torch.cuda.synchronize()
+
+    # kernel-only timing of the render launches (events on the launch stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record()
+        fr.launch()
+        ev[i][1].record()
+        fr.gather()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+        o = torch.tensor([float(ops_rank)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(o, op=dist.ReduceOp.SUM)
+        ops_total = float(o[0])
+    else:
+        kern_ms_max = kern_ms
+        ops_total = float(ops_rank)
+
+    if rank == 0:
+        frame_px = W * H
+        ms_step = elapsed / args.steps * 1e3
+        value = frame_px * args.steps / elapsed / 1e6
+        bytes_px = 12 if args.precision == "f32" else 24
+        # roofline of the dominant kernel (this rank's render launch), per launch
+        k_s = kern_ms / 1e3
+        valu_ach = ops_rank / k_s / 1e12
+        hbm_ach = px_rank * bytes_px / k_s / 1e9
+        wkey = f"{args.scene}-{W}x{H}-d{args.depth}-{args.order}-{args.precision}-n{world}"
+        tr = traffic_from_profiles(wkey)
+        line = {
+            "metric": "Mpixels/sec at 4096x4096, recursion depth 5 (frame rendered into HBM, gathered to rank 0)",
+            "value": round(value, 3),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"{args.scene.upper()} {W}x{H} depth {args.depth}", "scene": args.scene,
+                       "width": W, "height": H, "depth": args.depth, "order": args.order,
+                       "framebuffer": args.precision, "row_block": args.row_block,
+                       "parallelism": f"rows{world}" + ("+rccl_gather" if world > 1 else ""),
+                       "spheres": counts["spheres"], "triangles": counts["triangles"], "planes": counts["planes"],
+                       "lights": counts["lights"]},
+            "roofline": {"bound": "valu", "achieved": round(valu_ach, 3), "peak": PEAK_FP64_VALU_TOPS,
+                         "unit": "TFLOP/s", "frac": round(valu_ach / PEAK_FP64_VALU_TOPS, 4),
+                         "traffic": tr[0] if tr else None,
+                         "note": "FP64 VALU (binding): algorithmic binary64 ops per launch (SURVEY.md 8d weights, "
+                                 f"{ops_rank:.4g} ops for {px_rank} px) / mean render-launch time "
+                                 f"{kern_ms:.3f} ms; peak = 78.6 TFLOP/s FP64 vector / 2 (no FMA: contraction off)"
+                                 + (f"; traffic from {tr[1]}" if tr else "")},
+            "roofline_hbm": {"bound": "hbm", "achieved": round(hbm_ach, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": round(hbm_ach / PEAK_HBM_GBS, 6), "traffic": tr[0] if tr else None},
+            "kernel_ms": round(kern_ms, 4),
+            "kernel_ms_max_rank": round(kern_ms_max, 4),
+            "kernel_mpx_s": round(px_rank / k_s / 1e6, 3),
+            "ops_per_frame": ops_total,
+        }
+        if world == 1 and not args.no_boundary:
+            from eraytracer_amd.raytracer import render
+            st = {}
+            render(W, H, scene, args.depth, precision=args.precision, order=args.order, stats=st)
+            ts = []
+            for _ in range(2):
+                st = {}
+                render(W, H, scene, args.depth, precision=args.precision, order=args.order, stats=st)
+                ts.append(st["total_ms"])
+            line["boundary_mpx_s"] = round(frame_px / (min(ts) / 1e3) / 1e6, 3)
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(scene, W, H, args.depth, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    fr.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
