@@ -45,6 +45,20 @@ def test_render_matches_oracle(oracle, name, w, h, d):
     _check(img, ref)
 
 
+@pytest.mark.parametrize("idx", range(6))
+def test_tricky_scenes(oracle, idx):
+    """Duplicates (=:= copies light each other, 4 vs 4.0 copies shadow), no lights, stray
+    list elements, a triangle behind the camera (negative t wins), negative colours: the
+    any-hit shadow restatement and the type-grouped scans must keep the reference's answers."""
+    from tests.test_oracle import TRICKY
+    scene = TRICKY[idx]()
+    for d in (1, 3, 5):
+        img, lv = render(48, 36, scene, d, levels=True)
+        ref, rlv = _oracle(oracle, scene, 48, 36, d)
+        np.testing.assert_array_equal(lv, rlv)
+        _check(img, ref)
+
+
 @pytest.mark.parametrize("name,w,h,d", [("default", 64, 48, 5), ("s64", 48, 48, 5)])
 def test_fast_order_and_f32(oracle, name, w, h, d):
     scene = scenes.named(name)

@@ -1,0 +1,200 @@
+"""The oracle, pinned by the reference's own unit tests (raytracer.erl:735-1133, restated
+as known-answer tests) and by the committed golden vectors.
+
+Both restatements are checked: the C oracle (oracle/rt_oracle.c, which the GPU parity
+tests use) and the term-level Python restatement (oracle/erl_restatement.py).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from eraytracer_amd import _native as N
+from eraytracer_amd import records as R
+from eraytracer_amd import scenes, terms
+from oracle import erl_restatement as E
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def vectors_equal(a, b, eps=0.0001):  # raytracer.erl:513-521
+    return all(x + eps >= y and x - eps <= y for x, y in zip(a, b))
+
+
+# ---- scene_test/0 (raytracer.erl:760-801) ---------------------------------------------------
+SCENE_TEST_TERM = """
+[{camera, {vector, 0, 0, -2}, {vector, 0, 0, 0}, 90, {screen, 4, 3}},
+ {point_light, {colour, 1, 1, 0.5}, {vector, 5, -2, 0}, {colour, 1, 1, 1}},
+ {point_light, {colour, 1, 0, 0.5}, {vector, -10, 0, 7}, {colour, 1, 0, 0.5}},
+ {sphere, 4, {vector, 4, 0, 10}, {material, {colour, 0, 0.5, 1}, 20, 1, 0.1}},
+ {sphere, 4, {vector, -5, 3, 9}, {material, {colour, 1, 0.5, 0}, 4, 0.25, 0.5}},
+ {sphere, 4, {vector, -4.5, -2.5, 14}, {material, {colour, 0.5, 1, 0}, 20, 0.25, 0.7}},
+ {triangle, {vector, -2, 5, 5}, {vector, 4, 5, 10}, {vector, 4, -5, 10},
+  {material, {colour, 1, 0.5, 0}, 4, 0.25, 0.5}},
+ {plane, {vector, 0, -1, 0}, 5, {material, {colour, 1, 1, 1}, 1, 0, 0.01}}]
+"""
+
+
+def test_scene_test():
+    assert terms.exact_eq(R.scene(), terms.parse_term(SCENE_TEST_TERM))
+    assert terms.exact_eq(terms.consult(os.path.join(GOLDEN, "scene_default.eterm"))[0], R.scene())
+
+
+# ---- vector KATs (raytracer.erl:828-1000), C oracle and Python restatement -------------------
+def test_vector_kats(oracle):
+    O = oracle
+    assert O.vec_op("add", (3, 7, -3), (0, -24, 123)) == (3, -17, 120)              # :849-854
+    assert O.vec_op("add", (5, 0, 984), (5, 0, 984)) == (10, 0, 1968)               # :856-860
+    assert O.vec_op("square_mag", (3, -4, 0))[0] == 25                                # :893
+    assert O.vec_op("square_mag", (1, 1, 1))[0] == 3
+    assert O.vec_op("mag", (1, 1, 1))[0] == math.sqrt(3)                              # :904 exact
+    assert O.vec_op("mag", (3, -4, 0))[0] == 5
+    assert O.vec_op("mag", (0, 0, 0))[0] == 0
+    assert O.vec_op("dot", (1, 3, -5), (4, -2, -1))[0] == 3                           # :933
+    assert vectors_equal(O.vec_op("cross", (1, 2, 3), (4, 5, 6)), (-3, 6, -3))        # :956
+    assert vectors_equal(O.vec_op("cross", (0, 1, 0), (0, 0, 1)), (1, 0, 0))          # :955
+    assert vectors_equal(O.vec_op("normalize", (0, 0, 0)), (0, 0, 0))                 # :984
+    assert vectors_equal(O.vec_op("normalize", (5, 0, 0)), (1, 0, 0))                 # :986
+    assert vectors_equal(O.vec_op("normalize", (324, 0, 0)), (1, 0, 0))               # :987
+    assert vectors_equal(O.vec_op("neg", O.vec_op("neg", (4, -5, 6))), (4, -5, 6))    # :998
+    assert vectors_equal(O.vec_op("scalar_mult", (1, 1, 1), s=4), (4, 4, 4))          # :918
+    assert not vectors_equal(O.vec_op("scalar_mult", (3, -4, 0), s=-3), (3, -4, 0))   # :921
+    # Jacobi identity (:963-974)
+    a, b, c = (-3, 6, -3), (-1, 0, 0), (-9, 8, 433)
+    j = O.vec_op("add", O.vec_op("add", O.vec_op("cross", a, O.vec_op("cross", b, c)),
+                                 O.vec_op("cross", b, O.vec_op("cross", c, a))),
+                 O.vec_op("cross", c, O.vec_op("cross", a, b)))
+    assert vectors_equal(j, (0, 0, 0))
+    # Python restatement agrees
+    assert E.vector_dot_product(E.vec(1, 3, -5), E.vec(4, -2, -1)) == 3
+    assert E.vector_mag(E.vec(1, 1, 1)) == math.sqrt(3)
+    assert E.vectors_equal(E.vector_cross_product(E.vec(1, 2, 3), E.vec(4, 5, 6)), E.vec(-3, 6, -3))
+
+
+def test_bounce_kat(oracle):  # vector_bounce_off_plane_test/0 (:1115-1133)
+    O = oracle
+    assert vectors_equal(O.vec_op("bounce", (1, 1, 0), O.vec_op("normalize", (0, -1, 0))), (1, -1, 0))
+    assert vectors_equal(O.vec_op("bounce", (0, -1, 0), O.vec_op("normalize", (1, 1, 0))), (1, 0, 0))
+
+
+def test_ray_shooting_kat(oracle):  # ray_shooting_test/0 (:1002-1011)
+    assert vectors_equal(oracle.shoot_ray((0, 0, 0), (1, 0, 0)), (1, 0, 0))
+    assert E.vectors_equal(E.shoot_ray(E.vec(0, 0, 0), E.vec(1, 0, 0))[2], E.vec(1, 0, 0))
+
+
+def _elem(term):
+    return N.marshal([R.camera(R.vector(0, 0, 0), R.vector(0, 0, 0), 90, R.screen(1, 1)), term])[1]
+
+
+def test_ray_sphere_intersection_kat(oracle):  # ray_sphere_intersection_test/0 (:1013-1034)
+    # the reference's test sphere has `undefined` material fields; any material will do here
+    s = R.sphere(3, R.vector(0, 0, 10), R.material(R.colour(0.4, 0.4, 0.4), 1, 1, 0))
+    e = _elem(s)
+    hit = oracle.intersect(e, (0, 0, 0), (0, 0, 1))
+    assert hit is not None and hit[0] == 7.0                       # exact, :1031
+    assert oracle.intersect(e, (3, 0, 0), (0, 0, 1)) is None        # tangent: discriminant 0 < 0.001
+    assert oracle.intersect(e, (4, 0, 0), (0, 0, 1)) is None
+    ray1 = R.ray(R.vector(0, 0, 0), R.vector(0, 0, 1))
+    assert E.ray_sphere_intersect(ray1, s)[0] == 7.0
+    assert E.ray_sphere_intersect(R.ray(R.vector(3, 0, 0), R.vector(0, 0, 1)), s) is None
+    assert E.ray_sphere_intersect(R.ray(R.vector(4, 0, 0), R.vector(0, 0, 1)), s) is None
+
+
+def test_point_on_screen_kat(oracle):  # point_on_screen_test/0 (:1036-1066)
+    cams = [R.camera(R.vector(0, 0, 0), R.vector(0, 0, 0), 90, R.screen(1, 1)),
+            R.camera(R.vector(0, 0, 0), R.vector(0, 0, 0), 90, R.screen(640, 480))]
+    cases = [(0, 0.5, 0.5, (0, 0, 0.5)), (0, 0, 0, (-0.5, -0.5, 0.5)), (0, 1, 1, (0.5, 0.5, 0.5)),
+             (1, 0, 0, (-320, -240, 320)), (1, 1, 1, (320, 240, 320)), (1, 0.5, 0.5, (0, 0, 320))]
+    for ci, X, Y, want in cases:
+        e = N.marshal([cams[ci]])[0]
+        assert vectors_equal(oracle.point_on_screen(e, X, Y), want), (ci, X, Y)
+        assert E.vectors_equal(E.point_on_screen(X, Y, cams[ci]), E.vec(*want))
+
+
+def test_nearest_object_kat(oracle):  # nearest_object_intersecting_ray_test/0 (:1068-1097)
+    mat = lambda b: R.material(R.colour(0, 0, b), 1, 1, 0)  # noqa: E731
+    spheres = [R.sphere(5, R.vector(0, 0, 10), mat(0.03)), R.sphere(5, R.vector(0, 0, 20), mat(0.06)),
+               R.sphere(5, R.vector(0, 0, 30), mat(0.09)), R.sphere(5, R.vector(0, 0, -10), mat(-0.4))]
+    el = N.marshal([R.camera(R.vector(0, 0, 0), R.vector(0, 0, 0), 90, R.screen(1, 1))] + spheres)
+    objs = (N.RtElem * 4)(*el[1:])
+    i, dist, loc, normal = oracle.nearest(objs, (0, 0, 0), (0, 0, 1))
+    assert i == 0 and dist == 5
+    assert vectors_equal(normal, (0, 0, -1))
+    assert abs((loc[0] ** 2 + loc[1] ** 2 + (loc[2] - 10) ** 2) - 25) < 0.001  # point_on_sphere/2 (:603-607)
+    r = E.nearest_object_intersecting_ray(R.ray(R.vector(0, 0, 0), R.vector(0, 0, 1)), spheres)
+    assert terms.exact_eq(r[0], spheres[0]) and r[1] == 5
+
+
+def test_focal_length_kat(oracle):  # focal_length_test/0 (:1099-1113), arguments as the test passes them
+    for fl, dim in [(13, 108), (15, 100.4), (18, 90), (21, 81.2)]:
+        assert fl - 0.1 <= oracle.focal_length(dim, 36) <= fl + 0.1
+        assert fl - 0.1 <= E.focal_length(dim, 36) <= fl + 0.1
+    assert oracle.focal_length(90, 4) == 4 / (2 * math.tan(90 * (math.pi / 180) / 2))  # 2.0000000000000004
+
+
+# ---- whole images ---------------------------------------------------------------------------------
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.int64)
+
+
+@pytest.mark.parametrize("name,w,h,d", [("default", 40, 30, 5), ("s64", 24, 24, 5), ("s256", 12, 12, 6)])
+def test_literal_equals_memo(oracle, name, w, h, d):
+    el = N.marshal(scenes.named(name))
+    a = oracle.render(el, w, h, d, mode=oracle.LITERAL)
+    b = oracle.render(el, w, h, d, mode=oracle.MEMO)
+    assert np.array_equal(_bits(a), _bits(b))
+
+
+def _py(scene, w, h, d):
+    return np.array([p[1] for p in E.raytraced_pixel_list_simple(w, h, scene, d)]).reshape(h, w, 3)
+
+
+TRICKY = [
+    # duplicates: =:= copies count as the hit object in shadow_factor (:263)
+    lambda: R.scene() + [R.sphere(4, R.vector(4, 0, 10), R.material(R.colour(0, 0.5, 1), 20, 1, 0.1))],
+    # int vs float radius: NOT =:= (4 =/= 4.0), so the copy shadows the original
+    lambda: R.scene()[:3] + [R.sphere(4.0, R.vector(4, 0, 10), R.material(R.colour(0, 0.5, 1), 20, 1, 0.1))]
+    + R.scene()[3:],
+    # no lights: every hit is black, no reflection
+    lambda: [s for s in R.scene() if s[0] != "point_light"],
+    # a non-object element and a second camera inside the list are skipped (:357, :248)
+    lambda: R.scene()[:2] + [R.camera(R.vector(1, 1, 1), R.vector(0, 0, 0), 45, R.screen(2, 2)),
+                             (terms.Atom("fog"), 40)] + R.scene()[2:],
+    # a triangle that faces the camera and passes behind it (negative t wins, :442)
+    lambda: R.scene() + [R.triangle(R.vector(-3, -3, -5), R.vector(3, -3, -5), R.vector(0, 3, -5),
+                                    R.material(R.colour(0.2, 0.3, 0.4), 4, 0.5, 0.3))],
+    # negative colour components and zero shininess
+    lambda: R.scene()[:3] + [R.sphere(2, R.vector(0, 1, 6), R.material(R.colour(0, 0, -0.4), 1, 0, 0.9))]
+    + R.scene()[3:],
+]
+
+
+@pytest.mark.parametrize("mk", TRICKY)
+def test_c_oracle_equals_term_restatement(oracle, mk):
+    scene = mk()
+    el = N.marshal(scene)
+    for d in (1, 3):
+        a = oracle.render(el, 24, 18, d, mode=oracle.MEMO)
+        b = _py(scene, 24, 18, d)
+        assert np.array_equal(_bits(a), _bits(b)), f"depth {d}"
+
+
+def test_golden_vectors(oracle):
+    with open(os.path.join(GOLDEN, "MANIFEST.txt")) as f:
+        names = [ln.strip() for ln in f if ln.strip().endswith(".npz")]
+    assert names
+    for fn in names:
+        _, name, size, dd = fn[:-4].split("_")
+        w, h = map(int, size.split("x"))
+        d = int(dd[1:])
+        g = np.load(os.path.join(GOLDEN, fn))
+        img, lv = oracle.render(N.marshal(scenes.named(name)), w, h, d, mode=oracle.MEMO, levels=True)
+        assert np.array_equal(_bits(img), _bits(g["rgb"])), fn
+        assert np.array_equal(lv, g["levels"]), fn
+
+
+def test_golden_scene_files():
+    for name in ("default", "s64", "s256"):
+        t = terms.consult(os.path.join(GOLDEN, f"scene_{name}.eterm"))[0]
+        assert terms.exact_eq(t, scenes.named(name)), name
