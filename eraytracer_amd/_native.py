@@ -17,7 +17,7 @@ from .records import tag
 from .terms import exact_eq
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librtmi355x.so")
+LIB_PATH = os.environ.get("RT_LIB_PATH") or os.path.join(HERE, "librtmi355x.so")  # override: A/B builds
 
 RT_OK, RT_DONE, RT_EBADARG, RT_ENODEV, RT_EHIP, RT_ENOMEM, RT_ETOOBIG = 0, 1, -1, -2, -3, -4, -5
 RT_CAMERA, RT_POINT_LIGHT, RT_SPHERE, RT_TRIANGLE, RT_PLANE, RT_OTHER = range(6)

@@ -28,6 +28,16 @@ constexpr int PL_W = 4;      // nx ny nz distance
 constexpr int PL_ORG_W = 1;  // V0 = -(N.O + distance)          (:465-466)
 constexpr int OBJ_W = 12;    // n(3) or centre(3), colour(3), specular_power, shininess, reflectivity, pad
 constexpr int LIGHT_W = 12;  // diffuse(3), location(3), specular(3), pad(3)
+// wave culling (see rt_render.hip, "Beam culling"): sphere bounds and, per tabled origin, the
+// sphere's direction cone as seen from that origin with conservative margins applied
+constexpr int SPH_B_W = 4;   // cx cy cz r
+constexpr int SPH_OB_W = 8;  // vx vy vz (= c - o), |v|, sin(rho) upper bound, cos(rho) lower bound, near(0/1),
+                             // lower bound of |v| - r (no ray from o reaches the sphere before that distance)
+
+// Culling is exact only while every binary64 rounding error in the reference's sphere test is
+// far below its 0.001 discriminant threshold: all scene coordinates within this bound.
+constexpr double CULL_EXTENT = 1.0e4;
+constexpr double CULL_EPS = 1.0e-9; // angular / relative safety margin of the cull tests
 
 // int-table record widths (ints)
 constexpr int OBJ_META_W = 4; // kind, local index within its type, canon compact id, pad
@@ -38,10 +48,16 @@ enum ObjKind : int { K_SPHERE = 0, K_TRIANGLE = 1, K_PLANE = 2 };
 // or the int table `itab` (both device allocations owned by an rt_prepared).
 struct SceneHdr {
     int n_sph, n_tri, n_pl, n_obj, n_light, n_org; // n_org = 1 + n_light
+    int cull_ok;                                   // scene within CULL_EXTENT: beam culling allowed
+    int int_pow;                                   // every specular power is an integer in [0, 1024]
     // offsets into tab
-    int o_sph, o_sph_org, o_tri, o_tri_org, o_pl, o_pl_org, o_obj, o_light;
+    int o_sph, o_sph_org, o_tri, o_tri_org, o_pl, o_pl_org, o_obj, o_light, o_sph_b, o_sph_ob;
     // offsets into itab
     int i_sph_id, i_tri_id, i_pl_id, i_obj_meta;
+    // Occluder masks (only when cull_ok): for light i, target sphere t and 64-sphere chunk k,
+    // the uint64 at itab[i_occ + 2*((i*n_sph + t)*n_chunk + k)] has bit j set iff sphere
+    // 64k+j can block a shadow ray from light i to any point of sphere t (see rt_scene.cpp).
+    int i_occ, n_chunk;
     // camera (point_on_screen/3, :486-503, with focal_length/2 :483-484 folded in)
     double cam_x, cam_y, cam_z; // Camera#camera.location
     double sx;   // 0*F + Lx            (first fold step, x)

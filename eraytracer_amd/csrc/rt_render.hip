@@ -42,6 +42,16 @@ using namespace rtl;
 namespace {
 
 constexpr int BLOCK = 256; // 4 waves, 16x16 pixels
+
+// Occupancy target (waves per SIMD); the default is chosen by measurement.
+#ifndef RT_WAVES_PER_SIMD
+#define RT_WAVES_PER_SIMD 5
+#endif
+#if RT_WAVES_PER_SIMD > 0
+#define RT_LAUNCH_BOUNDS __launch_bounds__(256, RT_WAVES_PER_SIMD)
+#else
+#define RT_LAUNCH_BOUNDS __launch_bounds__(256)
+#endif
 constexpr int TILE = 16;
 
 struct D3 {
@@ -66,6 +76,36 @@ __device__ __forceinline__ D3 bounce3(const D3 &v, const D3 &n) { // vector_boun
 }
 
 __device__ __forceinline__ double max0(double x) { return x > 0 ? x : 0.0; } // lists:max([0, X])
+
+// math:pow/2 (:289) is the host libm's pow, which is correctly rounded for all but
+// vanishingly rare arguments.  For the small non-negative integer exponents scenes use
+// (specular_power 1, 4, 20) the kernel evaluates x^n by binary powering in double-double
+// arithmetic (~2^-100 relative error, then one rounding), which gives the correctly
+// rounded result — cheaper than, and closer to libm than, the device's general pow.  The
+// fma calls below are error-free product transformations, not contractions.
+__device__ __forceinline__ void dd_mul(double &ah, double &al, double bh, double bl) {
+    const double p = ah * bh;
+    double e = __builtin_fma(ah, bh, -p);
+    e = e + (ah * bl + al * bh);
+    const double s = p + e;
+    al = e - (s - p);
+    ah = s;
+}
+// GENPOW: the scene has a specular power outside {0, 1, ..., 1024} (decided on the host, see
+// pow_int_ok in rt_scene.cpp), so the general device pow is compiled in; otherwise its large
+// register footprint is kept out of the kernel.
+template <bool GENPOW>
+__device__ __forceinline__ double pow_libm(double x, double y) {
+    if (GENPOW && !(y >= 0.0 && y <= 1024.0 && y == __builtin_floor(y))) return pow(x, y);
+    unsigned n = (unsigned)y;
+    double rh = 1.0, rl = 0.0, bh = x, bl = 0.0;
+    while (n) {
+        if (n & 1u) dd_mul(rh, rl, bh, bl);
+        n >>= 1;
+        if (n) dd_mul(bh, bl, bh, bl);
+    }
+    return rh + rl;
+}
 
 // ---- primitive tests: return true and t on a valid hit --------------------------------------
 // ray_sphere_intersect/2 (:364-397), from B and C (A4 = 4*A hoisted per ray)
@@ -103,6 +143,20 @@ __device__ __forceinline__ bool pl_t(const D3 &n, const D3 &d, double V0, double
     return true;
 }
 
+// The same decision as sph_t without divergent branches: the root computation runs for the
+// whole wave unless no lane can hit (a wave-uniform test), and the outcome is a mask.
+__device__ __forceinline__ bool sph_t_wave(double B, double C, double A4, double &t) {
+    const double disc = B * B - A4 * C;
+    const bool ok = disc >= 0.001;
+    t = 0.0;
+    if (__ballot(ok) == 0) return false;
+    const double sq = sqrt(ok ? disc : 1.0);
+    const double t0 = (-B + sq) / 2;
+    const double t1 = (-B - sq) / 2;
+    t = (t1 < t0) ? t1 : t0;
+    return ok & (t0 >= 0) & (t1 >= 0);
+}
+
 __device__ __forceinline__ bool nearer(double t, int id, double bt, int bid) {
     return t < bt || (t == bt && id < bid); // first in list order among equal distances (:319)
 }
@@ -113,30 +167,194 @@ struct Scene {
     const int *__restrict__ itab;
 };
 
+// Diagnostic build only (-DRT_STATS): per-wave event counters read back with rt_debug_stats().
+#ifdef RT_STATS
+__device__ unsigned long long g_stats[16];
+#define RT_STAT(i, v)                                                                                              \
+    do {                                                                                                           \
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(&g_stats[i], (unsigned long long)(v));   \
+    } while (0)
+#else
+#define RT_STAT(i, v) \
+    do {              \
+    } while (0)
+#endif
+enum { ST_WAVES, ST_NEAR_PRE, ST_NEAR_PRE_CAND, ST_NEAR_GEN, ST_NEAR_GEN_CAND, ST_SHADOW, ST_SHADOW_CAND,
+       ST_SHADOW_ITER, ST_SHADE, ST_SHADOW_CONE_ON, ST_BEAM_ON, ST_SHADOW_LANES, ST_NEAR_LANES };
+
+// ---- Beam culling ----------------------------------------------------------------------------
+// A wave's 64 rays are coherent (an 8x8 pixel tile; shadow rays of one light; their
+// reflections).  Before a sphere scan the wave bounds its active rays by a cone of
+// directions (axis a, half-angle theta given by a lower bound c on cos and an upper bound s
+// on sin) around an origin ball (centre m, radius ro; ro = 0 for the camera and the
+// lights).  Lane j then tests sphere j of a 64-sphere chunk against that beam and a ballot
+// yields the chunk's candidate mask; the scan visits only candidates, with a wave-uniform
+// index (scalar loads).  A sphere is dropped only if its angular distance phi from the axis
+// exceeds theta + rho, rho = asin((r + ro) / |c - m|): then no ray of the beam comes within
+// r of the centre, and the reference's test (disc >= 0.001 and both roots >= 0, :378-381)
+// cannot succeed — its rounding error is < 1e-9 of the threshold for scenes within
+// CULL_EXTENT, and every bound below carries a CULL_EPS margin in the safe direction.
+// Wave reductions of binary64 values without LDS: four DPP steps reduce each 16-lane row
+// (quad_perm xor 1, xor 2, row_half_mirror, row_mirror — each an involution, so every lane
+// of a row ends with the same value), then the four row results are read into SGPRs.  The
+// wave must be converged (all 64 lanes active).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double lane_f64(double v, int lane) { // v of `lane`, in SGPRs
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((int)b, lane);
+    const unsigned hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+template <typename Op>
+__device__ __forceinline__ double wave_reduce(double v, Op op) {
+    v = op(v, dpp_f64<DPP_XOR1>(v));
+    v = op(v, dpp_f64<DPP_XOR2>(v));
+    v = op(v, dpp_f64<DPP_HALF_MIRROR>(v));
+    v = op(v, dpp_f64<DPP_MIRROR>(v));
+    return op(op(lane_f64(v, 0), lane_f64(v, 16)), op(lane_f64(v, 32), lane_f64(v, 48)));
+}
+__device__ __forceinline__ double wave_sum(double v) {
+    return wave_reduce(v, [](double a, double b) { return a + b; });
+}
+__device__ __forceinline__ double wave_min(double v) {
+    return wave_reduce(v, [](double a, double b) { return fmin(a, b); });
+}
+__device__ __forceinline__ double wave_max(double v) {
+    return wave_reduce(v, [](double a, double b) { return fmax(a, b); });
+}
+// every lane holds the same v: keep it in SGPRs
+__device__ __forceinline__ double uniform(double v) {
+    unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+struct Beam {
+    double ax, ay, az; // unit axis
+    double c, s;       // cos(theta) lower bound, sin(theta) upper bound
+    double mx, my, mz; // origin ball centre (unused when the origin is tabled)
+    double ro;         // origin ball radius
+    bool on;
+};
+
+// Must be called with the whole wave converged (it reduces across lanes).
+__device__ __forceinline__ Beam make_beam(const SceneHdr &h, bool act, const D3 &o, const D3 &d, bool fixed_origin) {
+    Beam b;
+    b.on = false;
+    b.ax = b.ay = b.az = b.c = b.s = b.mx = b.my = b.mz = b.ro = 0.0;
+    const unsigned long long am = __ballot(act);
+    if (!h.cull_ok || am == 0) return b;
+    const double sx = wave_sum(act ? d.x : 0.0), sy = wave_sum(act ? d.y : 0.0), sz = wave_sum(act ? d.z : 0.0);
+    const double n2 = uniform(sx * sx + sy * sy + sz * sz);
+    if (!(n2 > 0.0)) return b;
+    const double inv = 1.0 / sqrt(n2);
+    const double ax = uniform(sx * inv), ay = uniform(sy * inv), az = uniform(sz * inv);
+    const double dd = d.x * d.x + d.y * d.y + d.z * d.z;
+    const double idl = 1.0 / sqrt(dd);
+    const double cl = (ax * d.x + ay * d.y + az * d.z) * idl;
+    const double qx = ay * d.z - az * d.y, qy = az * d.x - ax * d.z, qz = ax * d.y - ay * d.x;
+    const double sl = sqrt(qx * qx + qy * qy + qz * qz) * idl;
+    const bool bad = act && !(dd > 0.25 && dd < 4.0); // degenerate direction: no culling
+    const double c = uniform(wave_min(act ? cl : 2.0)) - CULL_EPS;
+    const double s = uniform(wave_max(act ? sl : 0.0)) + CULL_EPS;
+    if (__ballot(bad) != 0 || !(c > 0.0)) return b; // cone wider than a hemisphere: scan everything
+    b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
+    if (!fixed_origin) {
+        const int first = __builtin_ctzll(am);
+        b.mx = lane_f64(o.x, first);
+        b.my = lane_f64(o.y, first);
+        b.mz = lane_f64(o.z, first);
+        const double ex = o.x - b.mx, ey = o.y - b.my, ez = o.z - b.mz;
+        const double r2 = wave_max(act ? ex * ex + ey * ey + ez * ez : 0.0);
+        const double mo = wave_max(act ? fmax(fabs(o.x), fmax(fabs(o.y), fabs(o.z))) : 0.0);
+        if (!(uniform(mo) <= CULL_EXTENT)) return b;
+        b.ro = uniform(sqrt(r2)) * (1 + CULL_EPS) + CULL_EPS;
+    }
+    b.on = true;
+    return b;
+}
+
+// Candidate mask of spheres [chunk, chunk+64): lane j tests sphere chunk+j against the beam.
+// org >= 0: the beam starts at tabled origin `org` (camera / light) and uses its cone table;
+// a sphere whose nearest surface point is farther than tmax from the origin is dropped too
+// (its hits have t > tmax; shadow scans only care about t <= t*, and t* <= tmax).
+__device__ __forceinline__ unsigned long long cull_chunk(const Scene &S, const Beam &b, int chunk, int org,
+                                                         double tmax = __builtin_inf()) {
+    // Branch-free: every load of the record is issued at once and the decision is a mask.
+    const SceneHdr &h = S.h;
+    const int k = chunk + (int)(threadIdx.x & 63);
+    const bool in = k < h.n_sph;
+    const int kk = in ? k : 0;
+    bool keep;
+    if (org >= 0) { // wave-uniform
+        const double2 *q = reinterpret_cast<const double2 *>(S.tab + h.o_sph_ob + (org * h.n_sph + kk) * SPH_OB_W);
+        const double2 q01 = q[0], q23 = q[1], q45 = q[2], q67 = q[3];
+        const double thr = b.c * q45.y - b.s * q45.x;                  // <= cos(theta + rho)
+        const double av = b.ax * q01.x + b.ay * q01.y + b.az * q23.x;  // |v| cos(phi)
+        keep = ((q67.x != 0.0) | !(av + CULL_EPS * q23.y < thr * q23.y)) & !(q67.y > tmax);
+    } else {
+        const double2 *g = reinterpret_cast<const double2 *>(S.tab + h.o_sph_b + kk * SPH_B_W);
+        const double2 g01 = g[0], g23 = g[1];
+        const double vx = g01.x - b.mx, vy = g01.y - b.my, vz = g23.x - b.mz;
+        const double vl = sqrt(vx * vx + vy * vy + vz * vz);
+        const double rp = g23.y + b.ro;
+        const double sr = rp / vl * (1 + CULL_EPS) + CULL_EPS;
+        const double cr = sqrt(fmax(1.0 - sr * sr, 0.0)) - CULL_EPS;
+        const double thr = b.c * cr - b.s * sr;
+        const double av = b.ax * vx + b.ay * vy + b.az * vz;
+        keep = (vl <= rp * (1 + CULL_EPS) + CULL_EPS) | (sr >= 1.0) | !(av + CULL_EPS * vl < thr * vl);
+    }
+    return __ballot(in & keep);
+}
+
+__device__ __forceinline__ unsigned long long chunk_all(int n_sph, int chunk) {
+    const int n = n_sph - chunk;
+    return n >= 64 ? ~0ull : ((1ull << n) - 1);
+}
+
 // nearest_object_intersecting_ray/6 (:303-346).  PRE: the ray starts at origin slot `org`
-// (tabled); otherwise at r_o.  Returns the compact object id (-1 = none) and its t.
+// (tabled); otherwise at o.  Returns the compact object id (-1 = none) and its t.
+// Called by the whole wave; `act` marks the lanes whose ray is traced.
 template <bool PRE>
-__device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt) {
+__device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, bool act) {
     const SceneHdr &h = S.h;
     bt = __builtin_inf();
     int bid = 0x7fffffff;
     const double A4 = 4 * (d.x * d.x + d.y * d.y + d.z * d.z);
-    for (int k = 0; k < h.n_sph; ++k) {
-        double B, C;
-        if (PRE) {
-            const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
-            B = 2 * (d.x * q[0] + d.y * q[1] + d.z * q[2]);
-            C = q[3];
-        } else {
-            const double *s = S.tab + h.o_sph + k * SPH_W;
-            D3 oc = {o.x - s[0], o.y - s[1], o.z - s[2]};
-            B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
-            C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - s[3];
-        }
-        double t;
-        if (sph_t(B, C, A4, t)) {
-            int id = S.itab[h.i_sph_id + k];
-            if (nearer(t, id, bt, bid)) { bt = t; bid = id; }
+    const Beam b = make_beam(h, act, o, d, PRE);
+    RT_STAT(PRE ? ST_NEAR_PRE : ST_NEAR_GEN, 1);
+    RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
+    RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
+    for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
+        unsigned long long m = b.on ? cull_chunk(S, b, chunk, PRE ? org : -1) : chunk_all(h.n_sph, chunk);
+        RT_STAT(PRE ? ST_NEAR_PRE_CAND : ST_NEAR_GEN_CAND, __popcll(m));
+        while (m) {
+            const int k = chunk + __builtin_ctzll(m);
+            m &= m - 1;
+            double B, C;
+            if (PRE) {
+                const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
+                B = 2 * (d.x * q[0] + d.y * q[1] + d.z * q[2]);
+                C = q[3];
+            } else {
+                const double *s = S.tab + h.o_sph + k * SPH_W;
+                D3 oc = {o.x - s[0], o.y - s[1], o.z - s[2]};
+                B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
+                C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - s[3];
+            }
+            const int id = S.itab[h.i_sph_id + k];
+            double t;
+            const bool upd = (int)sph_t_wave(B, C, A4, t) & (int)nearer(t, id, bt, bid);
+            bt = upd ? t : bt;
+            bid = upd ? id : bid;
         }
     }
     for (int k = 0; k < h.n_tri; ++k) {
@@ -167,7 +385,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
             if (nearer(t, id, bt, bid)) { bt = t; bid = id; }
         }
     }
-    return bid == 0x7fffffff ? -1 : bid;
+    return (act && bid != 0x7fffffff) ? bid : -1;
 }
 
 // Hit point and normal of object `id` at distance t (as computed inside the reference's
@@ -183,18 +401,90 @@ __device__ __forceinline__ void hit_geom(const Scene &S, int id, const D3 &o, co
         N = D3{r[0], r[1], r[2]};
 }
 
+// Bounding ball of the active lanes' hit points (centre = their centroid), shared by the
+// shadow cones of every light at this level.  Called by the converged wave.
+struct HitBall {
+    double cx, cy, cz, r;
+    bool on;
+};
+__device__ __forceinline__ HitBall make_hitball(const SceneHdr &h, bool act, const D3 &hit) {
+    HitBall hb;
+    hb.on = false;
+    hb.cx = hb.cy = hb.cz = hb.r = 0.0;
+    const unsigned long long am = __ballot(act);
+    if (!h.cull_ok || am == 0) return hb;
+    const double inv_n = 1.0 / (double)__popcll(am);
+    hb.cx = uniform(wave_sum(act ? hit.x : 0.0) * inv_n);
+    hb.cy = uniform(wave_sum(act ? hit.y : 0.0) * inv_n);
+    hb.cz = uniform(wave_sum(act ? hit.z : 0.0) * inv_n);
+    const double ex = hit.x - hb.cx, ey = hit.y - hb.cy, ez = hit.z - hb.cz;
+    const double r2 = wave_max(act ? ex * ex + ey * ey + ez * ez : 0.0);
+    const double mo = wave_max(act ? fmax(fabs(hit.x), fmax(fabs(hit.y), fabs(hit.z))) : 0.0);
+    if (!(mo <= CULL_EXTENT)) return hb;
+    hb.r = uniform(sqrt(r2)) * (1 + CULL_EPS) + CULL_EPS;
+    hb.on = true;
+    return hb;
+}
+
+// The cone of shadow-ray directions from light position Lp to the hit ball, and the largest
+// shadow-ray distance t* any lane can have (a target is hit no farther than its hit point).
+__device__ __forceinline__ Beam shadow_cone(const HitBall &hb, const D3 &Lp, double &tmax) {
+    Beam b;
+    b.on = false;
+    b.ax = b.ay = b.az = b.c = b.s = b.mx = b.my = b.mz = b.ro = 0.0;
+    tmax = __builtin_inf();
+    if (!hb.on) return b;
+    const double wx = hb.cx - Lp.x, wy = hb.cy - Lp.y, wz = hb.cz - Lp.z;
+    const double D = sqrt(wx * wx + wy * wy + wz * wz);
+    if (!(D > hb.r * (1 + CULL_EPS) + CULL_EPS)) return b; // light inside the ball
+    const double sr = hb.r / D * (1 + CULL_EPS) + CULL_EPS;
+    if (!(sr < 1.0)) return b;
+    const double inv = 1.0 / D;
+    b.ax = wx * inv; b.ay = wy * inv; b.az = wz * inv;
+    b.s = sr;
+    b.c = sqrt(1.0 - sr * sr) - CULL_EPS;
+    if (!(b.c > 0.0)) return b;
+    tmax = (D + hb.r) * (1 + CULL_EPS) + CULL_EPS;
+    b.on = true;
+    return b;
+}
+
 // shadow_factor/4 (:256-267) as the exact bounded any-hit test described at the top.
 // c = canonical compact id of the hit object, sd = normalize(Hit - Light).
-__device__ __forceinline__ bool lit_by(const Scene &S, int light, int c, const D3 &sd, bool active) {
+// The shadow target of a lane at one level: canonical id, its kind and index within its type,
+// and (wave-uniform) the sphere every shading lane shares, if there is one (-1 otherwise).
+struct Target {
+    int c, kind, loc, skip;
+};
+__device__ __forceinline__ Target make_target(const Scene &S, int c, bool active) {
+    const SceneHdr &h = S.h;
+    Target T;
+    T.c = c;
+    const int2 kl = *reinterpret_cast<const int2 *>(S.itab + h.i_obj_meta + c * OBJ_META_W);
+    T.kind = kl.x;
+    T.loc = kl.y;
+    T.skip = -1;
+    const unsigned long long am = __ballot(active);
+    if (am != 0) {
+        const int cu = __builtin_amdgcn_readlane(c, __builtin_ctzll(am));
+        if (__ballot(active && c != cu) == 0) { // uniform target: a sphere cannot block itself
+            const int2 u = *reinterpret_cast<const int2 *>(S.itab + h.i_obj_meta + cu * OBJ_META_W);
+            if (u.x == K_SPHERE) T.skip = u.y;
+        }
+    }
+    return T;
+}
+
+__device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &T, const D3 &sd, bool active,
+                                       const HitBall &hb, const D3 &Lp) {
     const SceneHdr &h = S.h;
     const int org = 1 + light;
+    const int c = T.c, kind = T.kind, loc = T.loc, skip = T.skip;
     const double A4 = 4 * (sd.x * sd.x + sd.y * sd.y + sd.z * sd.z);
     // t* of the target itself along the shadow ray
     double ts = 0;
     bool valid = false;
     if (active) {
-        const int kind = S.itab[h.i_obj_meta + c * OBJ_META_W + 0];
-        const int loc = S.itab[h.i_obj_meta + c * OBJ_META_W + 1];
         if (kind == K_SPHERE) {
             const double *q = S.tab + h.o_sph_org + (org * h.n_sph + loc) * SPH_ORG_W;
             double B = 2 * (sd.x * q[0] + sd.y * q[1] + sd.z * q[2]);
@@ -211,17 +501,45 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, int c, const D
     }
     bool blocked = !valid; // a target the shadow ray misses is never lit
     if (__all(blocked)) return false;
-    for (int k = 0; k < h.n_sph; ++k) {
-        if (!blocked) {
-            const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
-            double B = 2 * (sd.x * q[0] + sd.y * q[1] + sd.z * q[2]);
-            double t;
-            if (sph_t(B, q[3], A4, t)) {
-                int id = S.itab[h.i_sph_id + k];
-                blocked = t < ts || (t == ts && id < c);
+    // Candidate occluders.  Sphere targets: the union of the host-precomputed occluder masks of
+    // the wave's distinct targets (no reductions).  Otherwise the cone from the light to the
+    // hit ball of the wave, culled lane-parallel.
+    const bool sph_targets = h.cull_ok && __ballot(!blocked && kind != K_SPHERE) == 0;
+    double tmax = __builtin_inf();
+    Beam b;
+    b.on = false;
+    if (!sph_targets) b = shadow_cone(hb, Lp, tmax); // shadow rays all start at the light
+    RT_STAT(ST_SHADOW, 1);
+    RT_STAT(ST_SHADOW_CONE_ON, (sph_targets || b.on) ? 1 : 0);
+    for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
+        unsigned long long m;
+        if (sph_targets) {
+            m = 0;
+            const unsigned long long *occ = reinterpret_cast<const unsigned long long *>(
+                S.itab + h.i_occ + 2 * ((light * h.n_sph) * h.n_chunk + (chunk >> 6)));
+            unsigned long long rem = __ballot(!blocked);
+            while (rem) {
+                const int tl = __builtin_amdgcn_readlane(loc, __builtin_ctzll(rem));
+                rem &= ~__ballot(!blocked && loc == tl);
+                m |= occ[tl * h.n_chunk];
             }
+        } else {
+            m = b.on ? cull_chunk(S, b, chunk, org, tmax) : chunk_all(h.n_sph, chunk);
+            if (skip >= chunk && skip < chunk + 64) m &= ~(1ull << (skip - chunk));
         }
-        if (__all(blocked)) return false;
+        RT_STAT(ST_SHADOW_CAND, __popcll(m));
+        while (m) {
+            const int k = chunk + __builtin_ctzll(m);
+            m &= m - 1;
+            RT_STAT(ST_SHADOW_ITER, 1);
+            const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
+            const int id = S.itab[h.i_sph_id + k];
+            const double B = 2 * (sd.x * q[0] + sd.y * q[1] + sd.z * q[2]);
+            double t;
+            const bool hit = sph_t_wave(B, q[3], A4, t);
+            blocked = blocked | (hit & ((t < ts) | ((t == ts) & (id < c))));
+            if (__all(blocked)) return false;
+        }
     }
     for (int k = 0; k < h.n_tri; ++k) {
         if (!blocked) {
@@ -250,13 +568,20 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, int c, const D
 }
 
 // lighting_function/6 (:209-252) for one hit, with the (per-light identical) reflection R.
+template <bool GENPOW>
 __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D3 &hit, const D3 &N, const D3 &R,
                                     bool active) {
     const SceneHdr &h = S.h;
     const double *m = S.tab + h.o_obj + id * OBJ_W;
     const D3 mc = {m[3], m[4], m[5]};
     const double spow = m[6], shin = m[7];
-    const int c = S.itab[h.i_obj_meta + id * OBJ_META_W + 2];
+    const Target T = make_target(S, S.itab[h.i_obj_meta + id * OBJ_META_W + 2], active);
+    // the hit ball is only needed for non-sphere shadow targets (see lit_by)
+    HitBall hb;
+    hb.on = false;
+    hb.cx = hb.cy = hb.cz = hb.r = 0.0;
+    if (__ballot(active && T.kind != K_SPHERE) != 0) hb = make_hitball(h, active, hit);
+    RT_STAT(ST_SHADE, 1);
     D3 F = {0.0, 0.0, 0.0};
     for (int i = 0; i < h.n_light; ++i) {
         const double *L = S.tab + h.o_light + i * LIGHT_W;
@@ -267,20 +592,24 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
         const D3 diff = {mc.x * dd, mc.y * dd, mc.z * dd};
         // specular_term/7 (:285-297)
         const D3 hn = normalize3(D3{ln.x + -d.x, ln.y + -d.y, ln.z + -d.z});
-        const double sp = shin * pow(max0(dot3(hn, N)), spow);
+        const double sp = shin * pow_libm<GENPOW>(max0(dot3(hn, N)), spow);
         const D3 spec = {Sc.x * sp, Sc.y * sp, Sc.z * sp};
         const D3 con = {diff.x + spec.x, diff.y + spec.y, diff.z + spec.z};
+        // A lane whose light term Lc (x) con is exactly zero gets the same bits for lit = 0 and
+        // lit = 1 (the factor only multiplies signed zeros by 0 or 1): skip its shadow test.
+        const D3 lc = {Lc.x * con.x, Lc.y * con.y, Lc.z * con.z};
+        const bool need = active && !(lc.x == 0.0 && lc.y == 0.0 && lc.z == 0.0);
         // shadow ray direction normalize(Hit - Light) == -normalize(Light - Hit), bit for bit
-        const double lit = lit_by(S, i, c, D3{-ln.x, -ln.y, -ln.z}, active) ? 1.0 : 0.0;
-        F.x = F.x + (R.x + Lc.x * con.x * lit);
-        F.y = F.y + (R.y + Lc.y * con.y * lit);
-        F.z = F.z + (R.z + Lc.z * con.z * lit);
+        const double lit = lit_by(S, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp) ? 1.0 : 0.0;
+        F.x = F.x + (R.x + lc.x * lit);
+        F.y = F.y + (R.y + lc.y * lit);
+        F.z = F.z + (R.z + lc.z * lit);
     }
     return F;
 }
 
-template <int ORDER, int PREC, bool LEVELS>
-__global__ __launch_bounds__(BLOCK) void k_render(SceneHdr hdr, const double *__restrict__ tab,
+template <int ORDER, int PREC, bool LEVELS, bool GENPOW>
+__global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict__ tab,
                                                   const int *__restrict__ itab, int W, int H, int depth, int rb,
                                                   int shard, int nshards, int slab_rows, void *__restrict__ out,
                                                   uint8_t *__restrict__ levels) {
@@ -292,6 +621,7 @@ __global__ __launch_bounds__(BLOCK) void k_render(SceneHdr hdr, const double *__
     const bool inside = x < W && ly < slab_rows;
     const int gy = ((ly / rb) * nshards + shard) * rb + (ly % rb);
     const bool active = inside && gy < H;
+    RT_STAT(ST_WAVES, 1);
 
     // primary ray: ray_through_pixel/3 (:510-511) at {X/Width, Y/Height} (:112)
     const double X = (double)x / (double)W, Y = (double)gy / (double)H;
@@ -311,7 +641,7 @@ __global__ __launch_bounds__(BLOCK) void k_render(SceneHdr hdr, const double *__
         for (int k = 0; k < depth; ++k) {
             double t = 0;
             int id = -1;
-            if (alive) id = (k == 0) ? nearest<true>(S, 0, o, d, t) : nearest<false>(S, 0, o, d, t);
+            id = (k == 0) ? nearest<true>(S, 0, o, d, t, alive) : nearest<false>(S, 0, o, d, t, alive);
             if (id < 0) alive = false;
             if (alive) {
                 st[k * BLOCK + tid] = t;
@@ -328,8 +658,8 @@ __global__ __launch_bounds__(BLOCK) void k_render(SceneHdr hdr, const double *__
             if (__all(!alive)) break;
         }
         // backward: shade each level with the colour of the level below it (:216-247)
-        int maxlev = nlev;
-        for (int off = 32; off > 0; off >>= 1) maxlev = max(maxlev, __shfl_xor(maxlev, off));
+        int maxlev = 0;
+        while (maxlev < depth && __ballot(nlev > maxlev) != 0) ++maxlev; // wave-wide max level
         for (int m = 0; m < maxlev; ++m) {
             const int k = nlev - 1 - m;
             const bool on = k >= 0;
@@ -346,7 +676,7 @@ __global__ __launch_bounds__(BLOCK) void k_render(SceneHdr hdr, const double *__
             }
             const double refl = S.tab[hdr.o_obj + id * OBJ_W + 8];
             const D3 R = {col.x * refl, col.y * refl, col.z * refl};
-            const D3 F = shade(S, id, d2, hit, N, R, on);
+            const D3 F = shade<GENPOW>(S, id, d2, hit, N, R, on);
             if (on) col = F;
         }
     } else {
@@ -357,7 +687,7 @@ __global__ __launch_bounds__(BLOCK) void k_render(SceneHdr hdr, const double *__
         for (int k = 0; k < depth; ++k) {
             double t = 0;
             int id = -1;
-            if (alive) id = (k == 0) ? nearest<true>(S, 0, o, d, t) : nearest<false>(S, 0, o, d, t);
+            id = (k == 0) ? nearest<true>(S, 0, o, d, t, alive) : nearest<false>(S, 0, o, d, t, alive);
             if (id < 0) alive = false;
             D3 hit = cam, N = cam;
             if (alive) {
@@ -365,7 +695,7 @@ __global__ __launch_bounds__(BLOCK) void k_render(SceneHdr hdr, const double *__
                 hit_geom(S, id, o, d, t, hit, N);
             }
             if (__all(!alive)) break;
-            const D3 F = shade(S, alive ? id : 0, d, hit, N, D3{0.0, 0.0, 0.0}, alive);
+            const D3 F = shade<GENPOW>(S, alive ? id : 0, d, hit, N, D3{0.0, 0.0, 0.0}, alive);
             if (alive) {
                 col.x = col.x + w * F.x;
                 col.y = col.y + w * F.y;
@@ -423,16 +753,16 @@ struct DevGuard { // restore the caller's current device on scope exit
     }
 };
 
-template <int ORDER, int PREC>
+template <int ORDER, int PREC, bool GENPOW>
 int launch_t(const rt_prepared *p, int W, int H, int depth, int rb, int shard, int nshards, int slab_rows, void *out,
              uint8_t *levels, hipStream_t st) {
     dim3 grid((W + TILE - 1) / TILE, (slab_rows + TILE - 1) / TILE);
     size_t lds = ORDER == RT_ORDER_EXACT ? (size_t)depth * BLOCK * 12 : 0;
     if (levels)
-        hipLaunchKernelGGL((k_render<ORDER, PREC, true>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
+        hipLaunchKernelGGL((k_render<ORDER, PREC, true, GENPOW>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
                            H, depth, rb, shard, nshards, slab_rows, out, levels);
     else
-        hipLaunchKernelGGL((k_render<ORDER, PREC, false>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
+        hipLaunchKernelGGL((k_render<ORDER, PREC, false, GENPOW>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
                            H, depth, rb, shard, nshards, slab_rows, out, levels);
     HIPCHK(hipGetLastError());
     return RT_OK;
@@ -441,6 +771,20 @@ int launch_t(const rt_prepared *p, int W, int H, int depth, int rb, int shard, i
 } // namespace
 
 extern "C" {
+
+#ifdef RT_STATS
+// diagnostic builds only (not part of include/rt_mi355x.h)
+int rt_debug_stats(unsigned long long *out, int n, int reset) {
+    if (n > 16) n = 16;
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), n * sizeof(unsigned long long)));
+    if (reset) {
+        unsigned long long z[16] = {0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof(z)));
+    }
+    return RT_OK;
+}
+#endif
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
@@ -533,13 +877,17 @@ int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, u
     DevGuard g(p->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     int W = (int)width, H = (int)height, D = (int)depth, rb = (int)row_block, sh = (int)shard, ns = (int)nshards;
-    if (order == RT_ORDER_EXACT)
-        return precision == RT_OUT_F64
-                   ? launch_t<RT_ORDER_EXACT, RT_OUT_F64>(p, W, H, D, rb, sh, ns, (int)slab, d_out, d_levels, st)
-                   : launch_t<RT_ORDER_EXACT, RT_OUT_F32>(p, W, H, D, rb, sh, ns, (int)slab, d_out, d_levels, st);
-    return precision == RT_OUT_F64
-               ? launch_t<RT_ORDER_FAST, RT_OUT_F64>(p, W, H, D, rb, sh, ns, (int)slab, d_out, d_levels, st)
-               : launch_t<RT_ORDER_FAST, RT_OUT_F32>(p, W, H, D, rb, sh, ns, (int)slab, d_out, d_levels, st);
+    const int slab_rows = (int)slab;
+#define RT_DISPATCH(O, P)                                                                                          \
+    return p->hdr.int_pow ? launch_t<O, P, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)           \
+                          : launch_t<O, P, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)
+    if (order == RT_ORDER_EXACT) {
+        if (precision == RT_OUT_F64) RT_DISPATCH(RT_ORDER_EXACT, RT_OUT_F64);
+        RT_DISPATCH(RT_ORDER_EXACT, RT_OUT_F32);
+    }
+    if (precision == RT_OUT_F64) RT_DISPATCH(RT_ORDER_FAST, RT_OUT_F64);
+    RT_DISPATCH(RT_ORDER_FAST, RT_OUT_F32);
+#undef RT_DISPATCH
 }
 
 // Copy the blocks of one shard's slab to their rows in a row-major image.  dst_kind selects

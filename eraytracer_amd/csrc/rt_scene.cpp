@@ -187,6 +187,8 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
         }
     }
     // per-object shading records, by compact id
+    h.int_pow = 1;
+    while (t.size() % 2) t.push_back(0); // every later section starts 16-byte aligned
     h.o_obj = (int)t.size();
     for (int i : objs) {
         const rt_elem &o = e[i];
@@ -211,6 +213,8 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
             m = &o.u.plane.material;
             a = o.u.plane.normal.x; b = o.u.plane.normal.y; c = o.u.plane.normal.z;
         }
+        const double sp = m->specular_power;
+        if (!(sp >= 0.0 && sp <= 1024.0 && sp == std::floor(sp))) h.int_pow = 0;
         t.insert(t.end(), {a, b, c, m->colour.x, m->colour.y, m->colour.z, m->specular_power, m->shininess,
                            m->reflectivity, 0, 0, 0});
     }
@@ -219,6 +223,38 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
         const auto &L = e[li].u.point_light;
         t.insert(t.end(), {L.diffuse_colour.x, L.diffuse_colour.y, L.diffuse_colour.z, L.location.x, L.location.y,
                            L.location.z, L.specular_colour.x, L.specular_colour.y, L.specular_colour.z, 0, 0, 0});
+    }
+    // beam-culling tables (only consulted by the kernel when h.cull_ok); 16-byte aligned records
+    while (t.size() % 2) t.push_back(0);
+    h.o_sph_b = (int)t.size();
+    for (int i : sph) {
+        const auto &s = e[i].u.sphere;
+        t.insert(t.end(), {s.center.x, s.center.y, s.center.z, std::fabs(s.radius)});
+    }
+    h.o_sph_ob = (int)t.size();
+    for (const rt_vec3 &o : org) {
+        for (int i : sph) {
+            const auto &s = e[i].u.sphere;
+            double vx = s.center.x - o.x, vy = s.center.y - o.y, vz = s.center.z - o.z;
+            double vl = std::sqrt(vx * vx + vy * vy + vz * vz);
+            double r = std::fabs(s.radius);
+            double near = vl <= r * (1 + CULL_EPS) + CULL_EPS ? 1.0 : 0.0;
+            double sr = near ? 1.0 : r / vl * (1 + CULL_EPS) + CULL_EPS;
+            double cr = sr >= 1.0 ? 0.0 : std::sqrt(1 - sr * sr) - CULL_EPS;
+            if (sr >= 1.0) near = 1.0;
+            const double dlow = (vl - r) - CULL_EPS * (vl + r) - CULL_EPS;
+            t.insert(t.end(), {vx, vy, vz, vl, sr, cr, near, dlow});
+        }
+    }
+    {
+        double ext = 0;
+        auto grow = [&](double v) { ext = std::fmax(ext, std::fabs(v)); };
+        for (const rt_vec3 &o : org) { grow(o.x); grow(o.y); grow(o.z); }
+        for (int i : sph) {
+            const auto &s = e[i].u.sphere;
+            grow(s.center.x); grow(s.center.y); grow(s.center.z); grow(s.radius);
+        }
+        h.cull_ok = ext <= CULL_EXTENT ? 1 : 0;
     }
     if (t.empty()) t.push_back(0);
 
@@ -237,6 +273,58 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
         for (size_t q = 0; q < grp.size(); q++)
             if (grp[q] == i) local = (int)q;
         it.insert(it.end(), {kind, local, compact[root(e, i)], 0});
+    }
+    // Occluder masks, per (light, target sphere).  Shadow rays to a target sphere t start at the
+    // light L and point into the cone from L around ball(c_t, r_t); the target's own t* (its
+    // entry point) is at most |c_t - L|.  Sphere j can block such a ray only if (a) it meets that
+    // cone (angular test as in the kernel's beam culling, with CULL_EPS margins in the safe
+    // direction) and (b) some point of it is within |c_t - L| of L.  The target itself never
+    // blocks (its t equals t* and its list position is not earlier).
+    h.n_chunk = (h.n_sph + 63) / 64;
+    while (it.size() % 2) it.push_back(0);
+    h.i_occ = (int)it.size();
+    if (h.cull_ok && h.n_sph > 0) {
+        for (int li : lights) {
+            const rt_vec3 &L = e[li].u.point_light.location;
+            for (int ti : sph) {
+                const auto &T = e[ti].u.sphere;
+                const double ax = T.center.x - L.x, ay = T.center.y - L.y, az = T.center.z - L.z;
+                const double D = std::sqrt(ax * ax + ay * ay + az * az);
+                const double rt = std::fabs(T.radius);
+                const bool wide = !(D > rt * (1 + CULL_EPS) + CULL_EPS); // light inside the target
+                const double st = wide ? 1.0 : rt / D * (1 + CULL_EPS) + CULL_EPS;
+                const double ct = st >= 1.0 ? 0.0 : std::sqrt(1 - st * st) - CULL_EPS;
+                const double tmax = D * (1 + CULL_EPS) + CULL_EPS;
+                std::vector<uint64_t> m(h.n_chunk, 0);
+                for (size_t j = 0; j < sph.size(); j++) {
+                    if ((int)sph[j] == ti) continue;
+                    const auto &S = e[sph[j]].u.sphere;
+                    const double vx = S.center.x - L.x, vy = S.center.y - L.y, vz = S.center.z - L.z;
+                    const double vl = std::sqrt(vx * vx + vy * vy + vz * vz);
+                    const double r = std::fabs(S.radius);
+                    bool keep;
+                    if (wide || st >= 1.0 || !(ct > 0.0) || vl <= r * (1 + CULL_EPS) + CULL_EPS) {
+                        keep = true;
+                    } else {
+                        const double sr = r / vl * (1 + CULL_EPS) + CULL_EPS;
+                        if (sr >= 1.0) {
+                            keep = true;
+                        } else {
+                            const double cr = std::sqrt(1 - sr * sr) - CULL_EPS;
+                            const double thr = ct * cr - st * sr;
+                            const double av = (ax * vx + ay * vy + az * vz) / D;
+                            keep = !(av + CULL_EPS * vl < thr * vl);
+                        }
+                    }
+                    const double dlow = (vl - r) - CULL_EPS * (vl + r) - CULL_EPS;
+                    if (keep && !(dlow > tmax)) m[j / 64] |= 1ull << (j % 64);
+                }
+                for (uint64_t w : m) {
+                    it.push_back((int)(uint32_t)(w & 0xffffffffu));
+                    it.push_back((int)(uint32_t)(w >> 32));
+                }
+            }
+        }
     }
     if (it.empty()) it.push_back(0);
 
