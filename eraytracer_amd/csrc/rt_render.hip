@@ -320,42 +320,66 @@ __device__ __forceinline__ unsigned long long chunk_all(int n_sph, int chunk) {
     return n >= 64 ? ~0ull : ((1ull << n) - 1);
 }
 
-// nearest_object_intersecting_ray/6 (:303-346).  PRE: the ray starts at origin slot `org`
-// (tabled); otherwise at o.  Returns the compact object id (-1 = none) and its t.
-// Called by the whole wave; `act` marks the lanes whose ray is traced.
+// The sphere candidates in mask m of chunk `chunk`, folded into the running nearest (bt, bid).
 template <bool PRE>
-__device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, bool act) {
+__device__ __forceinline__ void scan_spheres(const Scene &S, int org, const D3 &o, const D3 &d, double A4, int chunk,
+                                             unsigned long long m, double &bt, int &bid) {
+    const SceneHdr &h = S.h;
+    RT_STAT(PRE ? ST_NEAR_PRE_CAND : ST_NEAR_GEN_CAND, __popcll(m));
+    while (m) {
+        const int k = chunk + __builtin_ctzll(m);
+        m &= m - 1;
+        double B, C;
+        if (PRE) {
+            const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
+            B = 2 * (d.x * q[0] + d.y * q[1] + d.z * q[2]);
+            C = q[3];
+        } else {
+            const double *s = S.tab + h.o_sph + k * SPH_W;
+            D3 oc = {o.x - s[0], o.y - s[1], o.z - s[2]};
+            B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
+            C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - s[3];
+        }
+        const int id = S.itab[h.i_sph_id + k];
+        double t;
+        const bool upd = (int)sph_t_wave(B, C, A4, t) & (int)nearer(t, id, bt, bid);
+        bt = upd ? t : bt;
+        bid = upd ? id : bid;
+    }
+}
+
+// nearest_object_intersecting_ray/6 (:303-346).  PRE: the ray starts at origin slot `org`
+// (tabled); otherwise at o, on object `grp` (the previous hit, or -1).  Returns the compact
+// object id (-1 = none) and its t.  Called by the whole wave; `act` marks the traced lanes.
+// Reflection rays are culled per group of lanes leaving the same object (at most
+// MAX_GROUPS beams, the last one covering every remaining lane): lanes on different objects
+// would otherwise share one wide beam.  Testing a sphere twice cannot change the nearest.
+constexpr int MAX_GROUPS = 3;
+template <bool PRE>
+__device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, bool act,
+                                       int grp = -1) {
     const SceneHdr &h = S.h;
     bt = __builtin_inf();
     int bid = 0x7fffffff;
     const double A4 = 4 * (d.x * d.x + d.y * d.y + d.z * d.z);
-    const Beam b = make_beam(h, act, o, d, PRE);
     RT_STAT(PRE ? ST_NEAR_PRE : ST_NEAR_GEN, 1);
-    RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
     RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
-    for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
-        unsigned long long m = b.on ? cull_chunk(S, b, chunk, PRE ? org : -1) : chunk_all(h.n_sph, chunk);
-        RT_STAT(PRE ? ST_NEAR_PRE_CAND : ST_NEAR_GEN_CAND, __popcll(m));
-        while (m) {
-            const int k = chunk + __builtin_ctzll(m);
-            m &= m - 1;
-            double B, C;
-            if (PRE) {
-                const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
-                B = 2 * (d.x * q[0] + d.y * q[1] + d.z * q[2]);
-                C = q[3];
-            } else {
-                const double *s = S.tab + h.o_sph + k * SPH_W;
-                D3 oc = {o.x - s[0], o.y - s[1], o.z - s[2]};
-                B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
-                C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - s[3];
-            }
-            const int id = S.itab[h.i_sph_id + k];
-            double t;
-            const bool upd = (int)sph_t_wave(B, C, A4, t) & (int)nearer(t, id, bt, bid);
-            bt = upd ? t : bt;
-            bid = upd ? id : bid;
+    unsigned long long rem = __ballot(act);
+    for (int g = 0; g < MAX_GROUPS && rem; ++g) {
+        bool sel = act;
+        if (!PRE) {
+            const int gv = __builtin_amdgcn_readlane(grp, __builtin_ctzll(rem));
+            sel = (g == MAX_GROUPS - 1) ? ((rem >> (threadIdx.x & 63)) & 1) != 0 : (act && grp == gv);
         }
+        rem = PRE ? 0ull : (rem & ~__ballot(sel));
+        const Beam b = make_beam(h, sel, o, d, PRE);
+        RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
+        for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
+            const unsigned long long m =
+                b.on ? cull_chunk(S, b, chunk, PRE ? org : -1) : chunk_all(h.n_sph, chunk);
+            scan_spheres<PRE>(S, org, o, d, A4, chunk, m, bt, bid);
+        }
+        if (!b.on) break; // everything was scanned
     }
     for (int k = 0; k < h.n_tri; ++k) {
         const double *g = S.tab + h.o_tri + k * TRI_W;
@@ -567,14 +591,16 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
     return !blocked;
 }
 
-// lighting_function/6 (:209-252) for one hit, with the (per-light identical) reflection R.
+// lighting_function/6 (:209-252) for one hit.  The reflection the reference adds for every
+// light is R = col * refl (col = colour of the level below); it is formed at each use — the
+// same operation on the same operands, so the same bits — which keeps fewer values live
+// across the shadow scans (register pressure sets this kernel's occupancy).  The material is
+// re-read per light for the same reason.
 template <bool GENPOW>
-__device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D3 &hit, const D3 &N, const D3 &R,
-                                    bool active) {
+__device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D3 &hit, const D3 &N, const D3 &col,
+                                    double refl, bool active) {
     const SceneHdr &h = S.h;
     const double *m = S.tab + h.o_obj + id * OBJ_W;
-    const D3 mc = {m[3], m[4], m[5]};
-    const double spow = m[6], shin = m[7];
     const Target T = make_target(S, S.itab[h.i_obj_meta + id * OBJ_META_W + 2], active);
     // the hit ball is only needed for non-sphere shadow targets (see lit_by)
     HitBall hb;
@@ -586,6 +612,9 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
     for (int i = 0; i < h.n_light; ++i) {
         const double *L = S.tab + h.o_light + i * LIGHT_W;
         const D3 Lc = {L[0], L[1], L[2]}, Lp = {L[3], L[4], L[5]}, Sc = {L[6], L[7], L[8]};
+        const double2 m34 = *reinterpret_cast<const double2 *>(m + 4), m67 = *reinterpret_cast<const double2 *>(m + 6);
+        const D3 mc = {m[3], m34.x, m34.y};
+        const double spow = m67.x, shin = m67.y;
         // diffuse_term/4 (:272-279)
         const D3 ln = normalize3(D3{Lp.x - hit.x, Lp.y - hit.y, Lp.z - hit.z});
         const double dd = max0(dot3(N, ln));
@@ -601,9 +630,9 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
         const bool need = active && !(lc.x == 0.0 && lc.y == 0.0 && lc.z == 0.0);
         // shadow ray direction normalize(Hit - Light) == -normalize(Light - Hit), bit for bit
         const double lit = lit_by(S, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp) ? 1.0 : 0.0;
-        F.x = F.x + (R.x + lc.x * lit);
-        F.y = F.y + (R.y + lc.y * lit);
-        F.z = F.z + (R.z + lc.z * lit);
+        F.x = F.x + (col.x * refl + lc.x * lit);
+        F.y = F.y + (col.y * refl + lc.y * lit);
+        F.z = F.z + (col.z * refl + lc.z * lit);
     }
     return F;
 }
@@ -638,11 +667,13 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
         // forward: the reflection chain's nearest-object scans
         D3 o = cam, d = d0;
         bool alive = active;
+        int prev = -1;
         for (int k = 0; k < depth; ++k) {
             double t = 0;
             int id = -1;
-            id = (k == 0) ? nearest<true>(S, 0, o, d, t, alive) : nearest<false>(S, 0, o, d, t, alive);
+            id = (k == 0) ? nearest<true>(S, 0, o, d, t, alive) : nearest<false>(S, 0, o, d, t, alive, prev);
             if (id < 0) alive = false;
+            prev = id;
             if (alive) {
                 st[k * BLOCK + tid] = t;
                 so[k * BLOCK + tid] = id;
@@ -675,8 +706,7 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
                 hit_geom(S, id, o2, d2, st[k * BLOCK + tid], hit, N);
             }
             const double refl = S.tab[hdr.o_obj + id * OBJ_W + 8];
-            const D3 R = {col.x * refl, col.y * refl, col.z * refl};
-            const D3 F = shade<GENPOW>(S, id, d2, hit, N, R, on);
+            const D3 F = shade<GENPOW>(S, id, d2, hit, N, col, refl, on);
             if (on) col = F;
         }
     } else {
@@ -684,18 +714,20 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
         D3 o = cam, d = d0;
         double w = 1.0;
         bool alive = active;
+        int prev = -1;
         for (int k = 0; k < depth; ++k) {
             double t = 0;
             int id = -1;
-            id = (k == 0) ? nearest<true>(S, 0, o, d, t, alive) : nearest<false>(S, 0, o, d, t, alive);
+            id = (k == 0) ? nearest<true>(S, 0, o, d, t, alive) : nearest<false>(S, 0, o, d, t, alive, prev);
             if (id < 0) alive = false;
+            prev = id;
             D3 hit = cam, N = cam;
             if (alive) {
                 nlev = k + 1;
                 hit_geom(S, id, o, d, t, hit, N);
             }
             if (__all(!alive)) break;
-            const D3 F = shade<GENPOW>(S, alive ? id : 0, d, hit, N, D3{0.0, 0.0, 0.0}, alive);
+            const D3 F = shade<GENPOW>(S, alive ? id : 0, d, hit, N, D3{0.0, 0.0, 0.0}, 0.0, alive);
             if (alive) {
                 col.x = col.x + w * F.x;
                 col.y = col.y + w * F.y;
