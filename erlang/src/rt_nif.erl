@@ -1,0 +1,19 @@
+%% rt_nif.erl — Erlang side of the NIF in erlang/c_src/rt_nif.c.
+-module(rt_nif).
+-export([render/5, render_binary/4]).
+-on_load(init/0).
+
+init() ->
+    Priv = case code:priv_dir(raytracer_gpu) of
+               {error, _} -> filename:join(filename:dirname(filename:dirname(code:which(?MODULE))), "priv");
+               Dir -> Dir
+           end,
+    erlang:load_nif(filename:join(Priv, "rt_nif"), 0).
+
+%% render(Width, Height, Scene, Depth, simple | indexed) -> done | [{Key, {R, G, B}}]
+render(_Width, _Height, _Scene, _Depth, _KeyMode) ->
+    erlang:nif_error(nif_not_loaded).
+
+%% render_binary(Width, Height, Scene, Depth) -> done | binary()
+render_binary(_Width, _Height, _Scene, _Depth) ->
+    erlang:nif_error(nif_not_loaded).
