@@ -29,7 +29,9 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -252,19 +254,26 @@ __device__ __forceinline__ Beam make_beam(const SceneHdr &h, bool act, const D3 
     b.ax = b.ay = b.az = b.c = b.s = b.mx = b.my = b.mz = b.ro = 0.0;
     const unsigned long long am = __ballot(act);
     if (!h.cull_ok || am == 0) return b;
-    const double sx = wave_sum(act ? d.x : 0.0), sy = wave_sum(act ? d.y : 0.0), sz = wave_sum(act ? d.z : 0.0);
-    const double n2 = uniform(sx * sx + sy * sy + sz * sz);
+    // Axis: the (normalised) direction of one active lane — the tile centre when it is active.
+    // Any axis inside the bundle gives a valid cone, at most twice as wide as the best one.
+    const int al = ((am >> 27) & 1) ? 27 : __builtin_ctzll(am);
+    const double rx = lane_f64(d.x, al), ry = lane_f64(d.y, al), rz = lane_f64(d.z, al);
+    const double n2 = rx * rx + ry * ry + rz * rz;
     if (!(n2 > 0.0)) return b;
-    const double inv = 1.0 / sqrt(n2);
-    const double ax = uniform(sx * inv), ay = uniform(sy * inv), az = uniform(sz * inv);
+    const double inv = uniform(1.0 / sqrt(n2));
+    const double ax = rx * inv, ay = ry * inv, az = rz * inv;
+    // The rays traced here are unit vectors to ~1e-15 (normalize/1 and bounces off unit
+    // normals).  Lanes are only required to have |d|^2 within DIR_TOL of 1, and the bounds are
+    // widened by 2*DIR_TOL instead of dividing by |d| (a plane normal that is not unit makes
+    // its reflections fail the check: that wave simply scans every sphere).
+    constexpr double DIR_TOL = 1.0e-6;
     const double dd = d.x * d.x + d.y * d.y + d.z * d.z;
-    const double idl = 1.0 / sqrt(dd);
-    const double cl = (ax * d.x + ay * d.y + az * d.z) * idl;
+    const double cl = ax * d.x + ay * d.y + az * d.z;
     const double qx = ay * d.z - az * d.y, qy = az * d.x - ax * d.z, qz = ax * d.y - ay * d.x;
-    const double sl = sqrt(qx * qx + qy * qy + qz * qz) * idl;
-    const bool bad = act && !(dd > 0.25 && dd < 4.0); // degenerate direction: no culling
-    const double c = uniform(wave_min(act ? cl : 2.0)) - CULL_EPS;
-    const double s = uniform(wave_max(act ? sl : 0.0)) + CULL_EPS;
+    const double sl = sqrt(qx * qx + qy * qy + qz * qz);
+    const bool bad = act && !(dd > 1.0 - DIR_TOL && dd < 1.0 + DIR_TOL);
+    const double c = uniform(wave_min(act ? cl : 2.0)) - CULL_EPS - 2 * DIR_TOL;
+    const double s = uniform(wave_max(act ? sl : 0.0)) + CULL_EPS + 2 * DIR_TOL;
     if (__ballot(bad) != 0 || !(c > 0.0)) return b; // cone wider than a hemisphere: scan everything
     b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
     if (!fixed_origin) {
@@ -361,6 +370,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
     const SceneHdr &h = S.h;
     bt = __builtin_inf();
     int bid = 0x7fffffff;
+    if (__ballot(act) == 0) return -1; // nothing to trace in this wave
     const double A4 = 4 * (d.x * d.x + d.y * d.y + d.z * d.z);
     RT_STAT(PRE ? ST_NEAR_PRE : ST_NEAR_GEN, 1);
     RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
@@ -600,6 +610,7 @@ template <bool GENPOW>
 __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D3 &hit, const D3 &N, const D3 &col,
                                     double refl, bool active) {
     const SceneHdr &h = S.h;
+    if (__ballot(active) == 0) return D3{0.0, 0.0, 0.0}; // no hit to shade in this wave
     const double *m = S.tab + h.o_obj + id * OBJ_W;
     const Target T = make_target(S, S.itab[h.i_obj_meta + id * OBJ_META_W + 2], active);
     // the hit ball is only needed for non-sphere shadow targets (see lit_by)
@@ -751,6 +762,8 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
     if (LEVELS) levels[pix] = (uint8_t)nlev;
 }
 
+#include "rt_wave.inc" // the wavefront engine (default)
+
 } // namespace
 
 // =====================================================================================
@@ -761,6 +774,15 @@ struct rt_prepared {
     SceneHdr hdr;
     double *d_tab;
     int *d_itab;
+    // wavefront-engine work space, grown on demand (one rt_launch in flight per rt_prepared)
+    void *d_queue = nullptr;  // HitRec[slab pixels * depth]
+    size_t queue_bytes = 0;
+    double *d_colbuf = nullptr; // chain colours, 3 doubles per level-0 hit
+    size_t colbuf_bytes = 0;
+    int *d_counts = nullptr;  // per level and tile: queue lengths
+    size_t counts_bytes = 0;
+    int *d_items = nullptr;   // per-level item counts, then per-level dense (tile, chunk) lists
+    size_t items_bytes = 0;
 };
 
 #define HIPCHK(x)                                                                                                  \
@@ -890,9 +912,122 @@ int rt_release(rt_prepared *p) {
     DevGuard g(p->device);
     (void)hipFree(p->d_tab);
     (void)hipFree(p->d_itab);
+    if (p->d_queue) (void)hipFree(p->d_queue);
+    if (p->d_colbuf) (void)hipFree(p->d_colbuf);
+    if (p->d_counts) (void)hipFree(p->d_counts);
+    if (p->d_items) (void)hipFree(p->d_items);
     delete p;
     return RT_OK;
 }
+
+} // extern "C"
+
+namespace {
+
+// Queue memory per pass is bounded (RT_QUEUE_MB, default 8 GiB); taller slabs are rendered
+// in several row passes.
+size_t queue_budget() {
+    static size_t b = [] {
+        const char *s = std::getenv("RT_QUEUE_MB");
+        size_t mb = s ? std::strtoull(s, nullptr, 10) : 8192;
+        return (mb < 64 ? 64 : mb) << 20;
+    }();
+    return b;
+}
+
+int grow(void **buf, size_t *have, size_t need) {
+    if (*have >= need) return RT_OK;
+    if (*buf) (void)hipFree(*buf);
+    *buf = nullptr;
+    *have = 0;
+    if (hipMalloc(buf, need) != hipSuccess) {
+        *buf = nullptr;
+        return RT_ENOMEM;
+    }
+    *have = need;
+    return RT_OK;
+}
+
+template <int PREC, bool GENPOW>
+int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns, int slab_rows, void *out,
+                     uint8_t *levels, hipStream_t st) {
+    const int nlev = D > 0 ? D : 1;
+    const size_t per_row = (size_t)W * nlev * sizeof(HitRec);
+    int pass_rows = (int)std::min<size_t>((size_t)slab_rows, std::max<size_t>(TILE, queue_budget() / per_row));
+    pass_rows = std::max(TILE, pass_rows / TILE * TILE);
+    if (pass_rows > slab_rows) pass_rows = slab_rows;
+    const int tiles_x = (W + TILE - 1) / TILE;
+    const size_t max_tiles = (size_t)tiles_x * ((pass_rows + TILE - 1) / TILE);
+    const size_t slots = max_tiles * TILE_SLOTS; // per level
+    int rc = grow(&p->d_queue, &p->queue_bytes, slots * nlev * sizeof(HitRec));
+    if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_colbuf), &p->colbuf_bytes, slots * 3 * sizeof(double));
+    if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_counts), &p->counts_bytes, max_tiles * nlev * sizeof(int));
+    // dense work lists: per level, (tile, chunk) items, then the item counts (one int per level)
+    const size_t items_ints = max_tiles * ITEMS_PER_TILE * nlev + 64;
+    if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_items), &p->items_bytes, items_ints * sizeof(int));
+    if (rc != RT_OK) return rc;
+    HitRec *q = static_cast<HitRec *>(p->d_queue);
+    const int nrefl = (p->hdr.n_light > 0 && D > 1) ? D - 1 : 0;
+    const int nshade = D > 0 ? 1 + nrefl : 0;
+    for (int row0 = 0; row0 < slab_rows; row0 += pass_rows) {
+        const int rows = std::min(pass_rows, slab_rows - row0);
+        const int ntiles = tiles_x * ((rows + TILE - 1) / TILE);
+        // the pass covers slab rows [row0, row0 + rows): out/levels offset to row0; the
+        // kernels map slab rows to image rows through the shard interleave themselves
+        const size_t off = (size_t)row0 * W;
+        void *o = static_cast<char *>(out) + off * 3 * (PREC == RT_OUT_F64 ? 8 : 4);
+        uint8_t *lv = levels ? levels + off : nullptr;
+        auto qk = [&](int k) { return q + (size_t)k * ntiles * TILE_SLOTS; };
+        auto ck = [&](int k) { return p->d_counts + (size_t)k * ntiles; };
+        int *nitems = p->d_items; // [0, 64): per-level item counts
+        auto ik = [&](int k) { return p->d_items + 64 + (size_t)k * ntiles * ITEMS_PER_TILE; };
+        HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
+        const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
+        dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
+        if (lv)
+            hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H, D,
+                               rb, sh, ns, rows, row0, o, lv, q, p->d_colbuf, p->d_counts, ntiles);
+        else
+            hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H,
+                               D, rb, sh, ns, rows, row0, o, lv, q, p->d_colbuf, p->d_counts, ntiles);
+        HIPCHK(hipGetLastError());
+        if (nshade > 0) {
+            hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(0), ntiles, ik(0), nitems + 0);
+            HIPCHK(hipGetLastError());
+        }
+        const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * ITEMS_PER_TILE + BLOCK / 64 - 1) / (BLOCK / 64));
+        for (int k = 1; k <= nrefl; ++k) {
+            if (lv)
+                hipLaunchKernelGGL((k_reflect<true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
+                                   k, ntiles, qk(k - 1), ck(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+            else
+                hipLaunchKernelGGL((k_reflect<false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
+                                   k, ntiles, qk(k - 1), ck(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+            HIPCHK(hipGetLastError());
+            hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k);
+            HIPCHK(hipGetLastError());
+        }
+        for (int k = nshade - 1; k >= 0; --k) {
+            hipLaunchKernelGGL((k_shade<PREC, GENPOW>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                               p->d_itab, k, ntiles, o, qk(k), ck(k), ik(k), nitems + k, p->d_colbuf);
+            HIPCHK(hipGetLastError());
+        }
+    }
+    return RT_OK;
+}
+
+// Engine: the wavefront pipeline (default) or the single fused kernel (RT_ENGINE=fused).
+bool use_mega_engine() {
+    static bool mega = [] {
+        const char *s = std::getenv("RT_ENGINE");
+        return s && (std::strcmp(s, "fused") == 0 || std::strcmp(s, "mega") == 0);
+    }();
+    return mega;
+}
+
+} // namespace
+
+extern "C" {
 
 int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, uint32_t row_block, uint32_t shard,
               uint32_t nshards, int precision, int order, void *d_out, uint8_t *d_levels, void *stream) {
@@ -910,6 +1045,15 @@ int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, u
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     int W = (int)width, H = (int)height, D = (int)depth, rb = (int)row_block, sh = (int)shard, ns = (int)nshards;
     const int slab_rows = (int)slab;
+    if (!use_mega_engine()) { // the wavefront engine always evaluates the reference's exact order
+        if (precision == RT_OUT_F64)
+            return p->hdr.int_pow
+                       ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)
+                       : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st);
+        return p->hdr.int_pow
+                   ? launch_wavefront<RT_OUT_F32, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)
+                   : launch_wavefront<RT_OUT_F32, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st);
+    }
 #define RT_DISPATCH(O, P)                                                                                          \
     return p->hdr.int_pow ? launch_t<O, P, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)           \
                           : launch_t<O, P, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)

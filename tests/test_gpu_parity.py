@@ -127,3 +127,30 @@ def test_full_size_sampled_rows(oracle):
         np.testing.assert_array_equal(lv[r0:r0 + 1], rlv)
         _check(img[r0:r0 + 1], ref)
     assert lv.max() <= 5
+
+
+def test_fused_engine_parity():
+    """The alternative single-kernel engine (RT_ENGINE=fused, chosen once per process) on the
+    same parity cases, run in a child process."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, sys\n"
+        "from eraytracer_amd import _native as N, scenes\n"
+        "from eraytracer_amd.raytracer import render\n"
+        "from oracle import oracle as O\n"
+        "from tests.test_oracle import TRICKY\n"
+        "cases = [(scenes.named(n), w, h, d) for n, w, h, d in [('default', 64, 48, 5), ('s64', 64, 64, 5),"
+        " ('s256', 40, 32, 8)]] + [(mk(), 40, 30, 3) for mk in TRICKY]\n"
+        "for order in ('exact', 'fast'):\n"
+        "    for sc, w, h, d in cases:\n"
+        "        img, lv = render(w, h, sc, d, levels=True, order=order)\n"
+        "        ref, rlv = O.render(N.marshal(sc), w, h, d, mode=O.MEMO, levels=True)\n"
+        "        assert np.array_equal(lv, rlv)\n"
+        "        assert np.abs(img - ref).max() <= 1e-5, (order, w, h, d)\n"
+        "print('fused ok')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RT_ENGINE="fused", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "fused ok" in r.stdout, r.stdout + r.stderr
