@@ -84,14 +84,20 @@ __device__ __forceinline__ double max0(double x) { return x > 0 ? x : 0.0; } // 
 // (specular_power 1, 4, 20) the kernel evaluates x^n by binary powering in double-double
 // arithmetic (~2^-100 relative error, then one rounding), which gives the correctly
 // rounded result — cheaper than, and closer to libm than, the device's general pow.  The
-// fma calls below are error-free product transformations, not contractions.
+// pairs hi + lo are kept unnormalised (|lo| stays within ~2 ulp(hi), the product's exact
+// low part plus the cross terms), so a step is one product and its fma error terms; the fma
+// calls are error-free product transformations, not contractions.
+__device__ __forceinline__ void dd_sqr(double &h, double &l) {
+    const double p = h * h;
+    const double e = __builtin_fma(h + h, l, __builtin_fma(h, h, -p));
+    h = p;
+    l = e;
+}
 __device__ __forceinline__ void dd_mul(double &ah, double &al, double bh, double bl) {
     const double p = ah * bh;
-    double e = __builtin_fma(ah, bh, -p);
-    e = e + (ah * bl + al * bh);
-    const double s = p + e;
-    al = e - (s - p);
-    ah = s;
+    const double e = __builtin_fma(al, bh, __builtin_fma(ah, bl, __builtin_fma(ah, bh, -p)));
+    ah = p;
+    al = e;
 }
 // GENPOW: the scene has a specular power outside {0, 1, ..., 1024} (decided on the host, see
 // pow_int_ok in rt_scene.cpp), so the general device pow is compiled in; otherwise its large
@@ -100,11 +106,16 @@ template <bool GENPOW>
 __device__ __forceinline__ double pow_libm(double x, double y) {
     if (GENPOW && !(y >= 0.0 && y <= 1024.0 && y == __builtin_floor(y))) return pow(x, y);
     unsigned n = (unsigned)y;
-    double rh = 1.0, rl = 0.0, bh = x, bl = 0.0;
-    while (n) {
-        if (n & 1u) dd_mul(rh, rl, bh, bl);
+    if (n == 0) return 1.0;
+    double bh = x, bl = 0.0;
+    while (!(n & 1u)) { // x^(2^k) for the lowest set bit: the result starts there
+        dd_sqr(bh, bl);
         n >>= 1;
-        if (n) dd_mul(bh, bl, bh, bl);
+    }
+    double rh = bh, rl = bl;
+    while (n >>= 1) {
+        dd_sqr(bh, bl);
+        if (n & 1u) dd_mul(rh, rl, bh, bl);
     }
     return rh + rl;
 }
@@ -548,15 +559,28 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
     for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
         unsigned long long m;
         if (sph_targets) {
-            m = 0;
+            // Every lane walks its own target's occluder mask: the trip count is the largest
+            // per-lane candidate count, not the size of the union over the wave's targets
+            // (which grows with every distinct target an incoherent wave holds).
             const unsigned long long *occ = reinterpret_cast<const unsigned long long *>(
                 S.itab + h.i_occ + 2 * ((light * h.n_sph) * h.n_chunk + (chunk >> 6)));
-            unsigned long long rem = __ballot(!blocked);
-            while (rem) {
-                const int tl = __builtin_amdgcn_readlane(loc, __builtin_ctzll(rem));
-                rem &= ~__ballot(!blocked && loc == tl);
-                m |= occ[tl * h.n_chunk];
+            unsigned long long mine = blocked ? 0ull : occ[loc * h.n_chunk]; // never holds the target
+            for (;;) {
+                const bool w = !blocked && mine != 0;
+                if (__ballot(w) == 0) break;
+                const int k = chunk + (w ? __builtin_ctzll(mine) : 0);
+                mine &= mine - 1;
+                RT_STAT(ST_SHADOW_ITER, 1);
+                const double2 *q = reinterpret_cast<const double2 *>(S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W);
+                const double2 q01 = q[0], q23 = q[1];
+                const int id = S.itab[h.i_sph_id + k];
+                const double B = 2 * (sd.x * q01.x + sd.y * q01.y + sd.z * q23.x);
+                double t;
+                const bool hit = sph_t_wave(B, q23.y, A4, t);
+                blocked = blocked | (w & hit & ((t < ts) | ((t == ts) & (id < c))));
             }
+            if (__all(blocked)) return false;
+            continue;
         } else {
             m = b.on ? cull_chunk(S, b, chunk, org, tmax) : chunk_all(h.n_sph, chunk);
             if (skip >= chunk && skip < chunk + 64) m &= ~(1ull << (skip - chunk));
@@ -781,7 +805,7 @@ struct rt_prepared {
     size_t colbuf_bytes = 0;
     int *d_counts = nullptr;  // per level and tile: queue lengths
     size_t counts_bytes = 0;
-    int *d_items = nullptr;   // per-level item counts, then per-level dense (tile, chunk) lists
+    int *d_items = nullptr;   // per-level record counts, then per-level dense slot lists
     size_t items_bytes = 0;
 };
 
@@ -962,8 +986,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     int rc = grow(&p->d_queue, &p->queue_bytes, slots * nlev * sizeof(HitRec));
     if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_colbuf), &p->colbuf_bytes, slots * 3 * sizeof(double));
     if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_counts), &p->counts_bytes, max_tiles * nlev * sizeof(int));
-    // dense work lists: per level, (tile, chunk) items, then the item counts (one int per level)
-    const size_t items_ints = max_tiles * ITEMS_PER_TILE * nlev + 64;
+    // dense work lists: 64 per-level record counts, then per level the slots of its records
+    const size_t items_ints = slots * nlev + 64;
     if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_items), &p->items_bytes, items_ints * sizeof(int));
     if (rc != RT_OK) return rc;
     HitRec *q = static_cast<HitRec *>(p->d_queue);
@@ -979,8 +1003,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         uint8_t *lv = levels ? levels + off : nullptr;
         auto qk = [&](int k) { return q + (size_t)k * ntiles * TILE_SLOTS; };
         auto ck = [&](int k) { return p->d_counts + (size_t)k * ntiles; };
-        int *nitems = p->d_items; // [0, 64): per-level item counts
-        auto ik = [&](int k) { return p->d_items + 64 + (size_t)k * ntiles * ITEMS_PER_TILE; };
+        int *nitems = p->d_items; // [0, 64): per-level record counts
+        auto ik = [&](int k) { return p->d_items + 64 + (size_t)k * ntiles * TILE_SLOTS; };
         HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
         dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
@@ -995,21 +1019,21 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(0), ntiles, ik(0), nitems + 0);
             HIPCHK(hipGetLastError());
         }
-        const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * ITEMS_PER_TILE + BLOCK / 64 - 1) / (BLOCK / 64));
+        const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
         for (int k = 1; k <= nrefl; ++k) {
             if (lv)
                 hipLaunchKernelGGL((k_reflect<true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
-                                   k, ntiles, qk(k - 1), ck(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+                                   k, ntiles, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
             else
                 hipLaunchKernelGGL((k_reflect<false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
-                                   k, ntiles, qk(k - 1), ck(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+                                   k, ntiles, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
             HIPCHK(hipGetLastError());
             hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k);
             HIPCHK(hipGetLastError());
         }
         for (int k = nshade - 1; k >= 0; --k) {
             hipLaunchKernelGGL((k_shade<PREC, GENPOW>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                               p->d_itab, k, ntiles, o, qk(k), ck(k), ik(k), nitems + k, p->d_colbuf);
+                               p->d_itab, k, ntiles, o, qk(k), ik(k), nitems + k, p->d_colbuf);
             HIPCHK(hipGetLastError());
         }
     }

@@ -1,88 +1,165 @@
 #!/usr/bin/env python3
-"""Summarise a scripts/profile.sh run (rocprofv3 kernel trace + PMC passes) for the render
-kernel into one JSON (profiles/<name>.json) that DESIGN.md and bench.py cite.
+"""Summarise a scripts/profile.sh run (rocprofv3 kernel trace + separate PMC passes) into one
+JSON (profiles/<name>.json) that DESIGN.md and bench.py cite.
 
     python scripts/pmc_summary.py gpurun_out/TAG profiles/r01_TAG_pmc.json WORKLOAD_KEY
 
-HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB, from separate
-passes; FETCH_SIZE under-reports wide coalesced streaming reads by 2x on gfx950 (this kernel
-reads only a few KiB of scene tables, so the read side is noted, not corrected); WRITE_SIZE is
-exact for 16-B-per-lane stores and uncalibrated for this kernel's 4-12-B stores.
+The unit is one FRAME LAUNCH (one rt_launch): the dispatch stream is cut into frames at each
+timed frame-start kernel (the wavefront engine's k_primary<PREC, false>, or the fused
+k_render<ORDER, PREC, false, ...>), and every render kernel up to the next non-render
+dispatch belongs to that frame.  The levels pass bench.py runs once (LEVELS=true variants) is
+excluded.  Counters are summed over a frame's kernels and averaged over frames; per-kernel
+entries are labelled name#i, i = occurrence within the frame (k_reflect#0 makes level 1,
+k_shade#0 shades the DEEPEST level).
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB and come from
+separate passes.  FETCH_SIZE under-reports wide coalesced streaming reads by 2x on gfx950; the
+hit-record queues are read with 64-B-per-lane loads, so the read side is reported raw and
+doubled (fetch_bytes_corrected); WRITE_SIZE is reported raw.
 """
 import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
+RENDER = re.compile(r"::(k_\w+)[<(]")
 
-def kernel_filter(name):
-    return "k_render" in name and "false>" in name  # the timed render variant (no levels output)
+
+def short(name):
+    m = RENDER.search(name)
+    return m.group(1) if m else None
+
+
+def frame_start(name):
+    return bool(re.search(r"k_primary<\d+, false>", name) or re.search(r"k_render<\d+, \d+, false", name))
+
+
+def frames(rows):
+    """rows: (dispatch_id, name, payload) in dispatch order -> list of frames, each a list of
+    (label, payload)."""
+    out, cur, seen = [], None, None
+    for _, name, payload in rows:
+        s = short(name)
+        if s and frame_start(name):
+            cur, seen = [], defaultdict(int)
+            out.append(cur)
+        elif s is None or (s in ("k_primary", "k_render")):
+            cur = None  # a non-render dispatch or the levels pass ends the frame
+            continue
+        if cur is None:
+            continue
+        cur.append((f"{s}#{seen[s]}", payload))
+        seen[s] += 1
+    return out
 
 
 def load_pmc(d):
-    vals = defaultdict(list)
+    per_disp = defaultdict(dict)
+    names = {}
     for f in glob.glob(os.path.join(d, "pmc*", "*counter_collection.csv")):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if kernel_filter(row["Kernel_Name"]):
-                    vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+                key = (os.path.dirname(f), int(row["Dispatch_Id"]))
+                per_disp[key][row["Counter_Name"]] = float(row["Counter_Value"])
+                names[key] = row["Kernel_Name"]
+    # each pmc pass is its own process: cut frames per pass, then average over all frames
+    tot, per_k, nfr = defaultdict(float), defaultdict(lambda: defaultdict(float)), defaultdict(int)
+    for pdir in sorted({k[0] for k in per_disp}):
+        rows = sorted(((k[1], names[k], per_disp[k]) for k in per_disp if k[0] == pdir))
+        fr = frames(rows)
+        for f in fr:
+            for label, c in f:
+                for cn, v in c.items():
+                    tot[cn] += v
+                    per_k[label][cn] += v
+            for cn in {cn for _, c in f for cn in c}:
+                nfr[cn] += 1
+    frame = {cn: tot[cn] / nfr[cn] for cn in tot if nfr[cn]}
+    kern = {lab: {cn: v / nfr[cn] for cn, v in c.items() if nfr[cn]} for lab, c in per_k.items()}
+    return frame, kern, dict(nfr)
 
 
 def load_trace(d):
-    f = glob.glob(os.path.join(d, "trace", "*kernel_stats.csv"))
+    f = glob.glob(os.path.join(d, "trace", "*kernel_trace.csv"))
     if not f:
-        return None
+        return None, None
+    rows = []
     with open(f[0]) as fh:
-        for row in csv.DictReader(fh):
-            if kernel_filter(row["Name"]):
-                return {"name": row["Name"], "calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
-                        "min_ns": float(row["MinNs"]), "max_ns": float(row["MaxNs"])}
-    return None
+        for r in csv.DictReader(fh):
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"],
+                         (int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["VGPR_Count"]))))
+    rows.sort()
+    fr = frames(rows)
+    if not fr:
+        return None, None
+    busy = [sum(e - s for _, (s, e, _) in f) for f in fr]
+    span = [f[-1][1][1] - f[0][1][0] for f in fr]
+    per = defaultdict(list)
+    vg = {}
+    for f in fr:
+        for lab, (s, e, v) in f:
+            per[lab].append(e - s)
+            vg[lab] = v
+    frame = {"frames": len(fr), "kernels_per_frame": len(fr[0]), "avg_busy_ns": sum(busy) / len(busy),
+             "avg_span_ns": sum(span) / len(span), "min_busy_ns": min(busy)}
+    kern = {lab: {"avg_ns": sum(v) / len(v), "vgpr": vg[lab]} for lab, v in per.items()}
+    return frame, kern
+
+
+def derive(c, ns):
+    d = {}
+    if c.get("SQ_WAVES"):
+        d["valu_insts_per_wave"] = c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"]
+    if c.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in c:
+        d["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"])
+    f64 = [c.get(k) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                              "SQ_INSTS_VALU_TRANS_F64")]
+    if all(v is not None for v in f64):
+        d["f64_wave_insts"] = sum(f64)
+        if c.get("SQ_INSTS_VALU"):
+            d["f64_share_of_valu"] = sum(f64) / c["SQ_INSTS_VALU"]
+        if ns:
+            # issue-slot view: every wave64 FP64 instruction occupies 64 lane-slots
+            d["f64_issue_frac_of_peak_39.3T"] = sum(f64) * 64 / (ns * 1e-9) / 39.3e12
+    if c.get("SQ_WAVE_CYCLES"):
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+            if k in c:
+                d[k.lower() + "_share"] = c[k] / c["SQ_WAVE_CYCLES"]
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        d["fetch_bytes"] = c["FETCH_SIZE"] * 1024
+        d["fetch_bytes_corrected"] = 2 * c["FETCH_SIZE"] * 1024
+        d["write_bytes"] = c["WRITE_SIZE"] * 1024
+    return d
 
 
 def main():
     src, dst, key = sys.argv[1], sys.argv[2], sys.argv[3]
-    pmc, n = load_pmc(src)
-    tr = load_trace(src)
-    out = {"workload": key, "source": os.path.basename(src.rstrip("/")), "kernel": tr, "counters": pmc,
-           "dispatches_per_counter": n}
-    d = {}
-    if "SQ_INSTS_VALU" in pmc and "SQ_WAVES" in pmc:
-        d["valu_insts_per_wave"] = pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"]
-    if "SQ_THREAD_CYCLES_VALU" in pmc and "SQ_ACTIVE_INST_VALU" in pmc and pmc["SQ_ACTIVE_INST_VALU"]:
-        d["valu_lane_utilisation"] = pmc["SQ_THREAD_CYCLES_VALU"] / (64 * pmc["SQ_ACTIVE_INST_VALU"])
-    f64 = [pmc.get(c) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
-                                "SQ_INSTS_VALU_TRANS_F64")]
-    if all(v is not None for v in f64):
-        d["f64_wave_insts"] = sum(f64)
-        d["f64_share_of_valu"] = sum(f64) / pmc["SQ_INSTS_VALU"] if pmc.get("SQ_INSTS_VALU") else None
-        if tr:
-            # issue-slot view: every wave64 FP64 instruction occupies 64 lane-slots
-            d["f64_lane_slots_per_s"] = sum(f64) * 64 / (tr["avg_ns"] * 1e-9)
-            d["f64_issue_frac_of_peak_39.3T"] = d["f64_lane_slots_per_s"] / 39.3e12
-    if "SQ_INSTS_VALU_FLOPS_FP64" in pmc and tr:
-        d["fp64_flops_per_s"] = pmc["SQ_INSTS_VALU_FLOPS_FP64"] / (tr["avg_ns"] * 1e-9)
-    if "GRBM_GUI_ACTIVE" in pmc and tr:
-        d["effective_clock_ghz"] = pmc["GRBM_GUI_ACTIVE"] / 8 / tr["avg_ns"]
-    if "SQ_WAVE_CYCLES" in pmc:
-        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
-            if k in pmc:
-                d[k.lower() + "_share"] = pmc[k] / pmc["SQ_WAVE_CYCLES"]
-    fetch = pmc.get("FETCH_SIZE")
-    write = pmc.get("WRITE_SIZE")
-    if fetch is not None and write is not None:
-        d["fetch_bytes"] = fetch * 1024
-        d["write_bytes"] = write * 1024
-        out["hbm_bytes_per_launch"] = (fetch + write) * 1024
-    out["derived"] = d
+    pmc, pmc_k, nfr = load_pmc(src)
+    tr, tr_k = load_trace(src)
+    out = {"workload": key, "source": os.path.basename(src.rstrip("/")), "unit": "one frame launch",
+           "trace": tr, "counters": pmc, "frames_per_counter": nfr,
+           "derived": derive(pmc, tr["avg_busy_ns"] if tr else None), "kernels": {}}
+    for lab in sorted(set(pmc_k) | set(tr_k or {}), key=lambda s: (s.split("#")[0], int(s.split("#")[1]))):
+        ent = dict((tr_k or {}).get(lab, {}))
+        ent["counters"] = pmc_k.get(lab, {})
+        ent["derived"] = derive(ent["counters"], ent.get("avg_ns"))
+        out["kernels"][lab] = ent
+    dd = out["derived"]
+    if "fetch_bytes" in dd:
+        out["hbm_bytes_per_launch"] = dd["fetch_bytes_corrected"] + dd["write_bytes"]
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
-    print(json.dumps({"kernel": tr, "derived": d, "hbm_bytes_per_launch": out.get("hbm_bytes_per_launch")},
+    print(json.dumps({"trace": tr, "derived": dd, "hbm_bytes_per_launch": out.get("hbm_bytes_per_launch")},
                      indent=1))
+    for lab, e in out["kernels"].items():
+        x = e["derived"]
+        print(f"{lab:14s} {e.get('avg_ns', 0) / 1e3:8.1f} us vgpr={e.get('vgpr')} "
+              f"valu/wave={x.get('valu_insts_per_wave', 0):8.0f} f64frac={x.get('f64_issue_frac_of_peak_39.3T', 0):.3f} "
+              f"valu_share={x.get('sq_active_inst_valu_share', 0):.3f} lanes={x.get('valu_lane_utilisation', 0):.2f}")
 
 
 if __name__ == "__main__":
