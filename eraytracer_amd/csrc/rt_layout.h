@@ -40,7 +40,7 @@ constexpr double CULL_EXTENT = 1.0e4;
 constexpr double CULL_EPS = 1.0e-9; // angular / relative safety margin of the cull tests
 
 // int-table record widths (ints)
-constexpr int OBJ_META_W = 4; // kind, local index within its type, canon compact id, pad
+constexpr int OBJ_META_W = 4; // kind, local index within its type, canon compact id, canon's local index
 
 enum ObjKind : int { K_SPHERE = 0, K_TRIANGLE = 1, K_PLANE = 2 };
 

@@ -501,21 +501,20 @@ __device__ __forceinline__ Beam shadow_cone(const HitBall &hb, const D3 &Lp, dou
 struct Target {
     int c, kind, loc, skip;
 };
-__device__ __forceinline__ Target make_target(const Scene &S, int c, bool active) {
-    const SceneHdr &h = S.h;
+__device__ __forceinline__ Target make_target(const Scene &S, int obj, bool active) {
+    // one row: kind, local, canonical id, the canonical element's local index (same kind)
+    const int4 mt = *reinterpret_cast<const int4 *>(S.itab + S.h.i_obj_meta + obj * OBJ_META_W);
     Target T;
-    T.c = c;
-    const int2 kl = *reinterpret_cast<const int2 *>(S.itab + h.i_obj_meta + c * OBJ_META_W);
-    T.kind = kl.x;
-    T.loc = kl.y;
+    T.c = mt.z;
+    T.kind = mt.x;
+    T.loc = mt.w;
     T.skip = -1;
     const unsigned long long am = __ballot(active);
     if (am != 0) {
-        const int cu = __builtin_amdgcn_readlane(c, __builtin_ctzll(am));
-        if (__ballot(active && c != cu) == 0) { // uniform target: a sphere cannot block itself
-            const int2 u = *reinterpret_cast<const int2 *>(S.itab + h.i_obj_meta + cu * OBJ_META_W);
-            if (u.x == K_SPHERE) T.skip = u.y;
-        }
+        const int first = __builtin_ctzll(am);
+        const int cu = __builtin_amdgcn_readlane(T.c, first);
+        if (__ballot(active && T.c != cu) == 0 && __builtin_amdgcn_readlane(T.kind, first) == K_SPHERE)
+            T.skip = __builtin_amdgcn_readlane(T.loc, first); // uniform target: a sphere cannot block itself
     }
     return T;
 }
@@ -630,13 +629,15 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
 // same operation on the same operands, so the same bits — which keeps fewer values live
 // across the shadow scans (register pressure sets this kernel's occupancy).  The material is
 // re-read per light for the same reason.
+// bits (optional): bit i set where light i's shadow test passed (lights 0..31; only lanes whose
+// light term is not exactly zero are tested, the others' bits are 0 and never matter).
 template <bool GENPOW>
 __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D3 &hit, const D3 &N, const D3 &col,
-                                    double refl, bool active) {
+                                    double refl, bool active, unsigned *bits = nullptr) {
     const SceneHdr &h = S.h;
     if (__ballot(active) == 0) return D3{0.0, 0.0, 0.0}; // no hit to shade in this wave
     const double *m = S.tab + h.o_obj + id * OBJ_W;
-    const Target T = make_target(S, S.itab[h.i_obj_meta + id * OBJ_META_W + 2], active);
+    const Target T = make_target(S, id, active);
     // the hit ball is only needed for non-sphere shadow targets (see lit_by)
     HitBall hb;
     hb.on = false;
@@ -664,7 +665,9 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
         const D3 lc = {Lc.x * con.x, Lc.y * con.y, Lc.z * con.z};
         const bool need = active && !(lc.x == 0.0 && lc.y == 0.0 && lc.z == 0.0);
         // shadow ray direction normalize(Hit - Light) == -normalize(Light - Hit), bit for bit
-        const double lit = lit_by(S, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp) ? 1.0 : 0.0;
+        const bool lb = lit_by(S, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp);
+        if (bits && lb && i < 32) *bits |= 1u << i;
+        const double lit = lb ? 1.0 : 0.0;
         F.x = F.x + (col.x * refl + lc.x * lit);
         F.y = F.y + (col.y * refl + lc.y * lit);
         F.z = F.z + (col.z * refl + lc.z * lit);
@@ -801,12 +804,25 @@ struct rt_prepared {
     // wavefront-engine work space, grown on demand (one rt_launch in flight per rt_prepared)
     void *d_queue = nullptr;  // HitRec[slab pixels * depth]
     size_t queue_bytes = 0;
-    double *d_colbuf = nullptr; // chain colours, 3 doubles per level-0 hit
+    double *d_colbuf = nullptr; // colours of levels 1 .. depth-1, 3 doubles per slot
     size_t colbuf_bytes = 0;
     int *d_counts = nullptr;  // per level and tile: queue lengths
     size_t counts_bytes = 0;
     int *d_items = nullptr;   // per-level record counts, then per-level dense slot lists
     size_t items_bytes = 0;
+    // the shadow pass runs on a second, low-priority stream beside the reflection chain
+    hipStream_t side[2] = {};  // level 0's shading; the deeper levels' shading
+    hipEvent_t ev_level[RT_MAX_DEPTH + 1] = {};
+    hipEvent_t ev_join[2] = {};
+    // Frames repeat with identical arguments (bench, multi-GPU renderer): the second identical
+    // rt_launch captures the frame's launch sequence into a graph, later ones replay it.
+    // gen counts work-space reallocations, which invalidate captured pointers.
+    unsigned gen = 0;
+    hipStream_t cap = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    long long gkey[12] = {};
+    long long last_key[12] = {};
+    bool last_valid = false;
 };
 
 #define HIPCHK(x)                                                                                                  \
@@ -940,6 +956,14 @@ int rt_release(rt_prepared *p) {
     if (p->d_colbuf) (void)hipFree(p->d_colbuf);
     if (p->d_counts) (void)hipFree(p->d_counts);
     if (p->d_items) (void)hipFree(p->d_items);
+    for (hipEvent_t &e : p->ev_level)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t &e : p->ev_join)
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t &x : p->side)
+        if (x) (void)hipStreamDestroy(x);
+    if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
+    if (p->cap) (void)hipStreamDestroy(p->cap);
     delete p;
     return RT_OK;
 }
@@ -959,8 +983,28 @@ size_t queue_budget() {
     return b;
 }
 
-int grow(void **buf, size_t *have, size_t need) {
+// RT_LIT_STREAM=0 keeps the shading pass on the caller's stream (no overlap), for A/B runs.
+bool lit_overlap() {
+    static bool on = [] {
+        const char *s = std::getenv("RT_LIT_STREAM");
+        return !(s && std::strcmp(s, "0") == 0);
+    }();
+    return on;
+}
+
+int side_stream(rt_prepared *p) {
+    if (p->side[0]) return RT_OK;
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    for (hipStream_t &x : p->side) HIPCHK(hipStreamCreateWithPriority(&x, hipStreamNonBlocking, least));
+    for (hipEvent_t &e : p->ev_level) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t &e : p->ev_join) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return RT_OK;
+}
+
+int grow(void **buf, size_t *have, size_t need, unsigned *gen) {
     if (*have >= need) return RT_OK;
+    ++*gen;
     if (*buf) (void)hipFree(*buf);
     *buf = nullptr;
     *have = 0;
@@ -983,13 +1027,23 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     const int tiles_x = (W + TILE - 1) / TILE;
     const size_t max_tiles = (size_t)tiles_x * ((pass_rows + TILE - 1) / TILE);
     const size_t slots = max_tiles * TILE_SLOTS; // per level
-    int rc = grow(&p->d_queue, &p->queue_bytes, slots * nlev * sizeof(HitRec));
-    if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_colbuf), &p->colbuf_bytes, slots * 3 * sizeof(double));
-    if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_counts), &p->counts_bytes, max_tiles * nlev * sizeof(int));
+    int rc = grow(&p->d_queue, &p->queue_bytes, slots * nlev * sizeof(HitRec), &p->gen);
+    // colours of levels 1 .. depth-1, 3 doubles per slot (level 0 goes straight to the frame)
+    const size_t col_doubles = slots * 3 * (size_t)std::max(1, nlev - 1);
+    if (rc == RT_OK)
+        rc = grow(reinterpret_cast<void **>(&p->d_colbuf), &p->colbuf_bytes, col_doubles * sizeof(double), &p->gen);
+    if (rc == RT_OK)
+        rc = grow(reinterpret_cast<void **>(&p->d_counts), &p->counts_bytes, max_tiles * nlev * sizeof(int), &p->gen);
     // dense work lists: 64 per-level record counts, then per level the slots of its records
     const size_t items_ints = slots * nlev + 64;
-    if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_items), &p->items_bytes, items_ints * sizeof(int));
+    if (rc == RT_OK)
+        rc = grow(reinterpret_cast<void **>(&p->d_items), &p->items_bytes, items_ints * sizeof(int), &p->gen);
+    const bool overlap = lit_overlap() && D > 1 && p->hdr.n_light > 0;
+    if (rc == RT_OK && overlap) rc = side_stream(p);
     if (rc != RT_OK) return rc;
+    // streams of the shading pass: level 0 (the bulk) beside the whole reflection chain, the
+    // deeper levels on a second stream so they need not wait for level 0's shading
+    auto ls = [&](int k) { return overlap ? p->side[k > 0 ? 1 : 0] : st; };
     HitRec *q = static_cast<HitRec *>(p->d_queue);
     const int nrefl = (p->hdr.n_light > 0 && D > 1) ? D - 1 : 0;
     const int nshade = D > 0 ? 1 + nrefl : 0;
@@ -1005,38 +1059,115 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         auto ck = [&](int k) { return p->d_counts + (size_t)k * ntiles; };
         int *nitems = p->d_items; // [0, 64): per-level record counts
         auto ik = [&](int k) { return p->d_items + 64 + (size_t)k * ntiles * TILE_SLOTS; };
+        auto colk = [&](int k) { return k > 0 ? p->d_colbuf + (size_t)(k - 1) * ntiles * TILE_SLOTS * 3 : nullptr; };
         HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
         dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
         if (lv)
             hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H, D,
-                               rb, sh, ns, rows, row0, o, lv, q, p->d_colbuf, p->d_counts, ntiles);
+                               rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles);
         else
             hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H,
-                               D, rb, sh, ns, rows, row0, o, lv, q, p->d_colbuf, p->d_counts, ntiles);
+                               D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles);
         HIPCHK(hipGetLastError());
-        if (nshade > 0) {
-            hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(0), ntiles, ik(0), nitems + 0);
-            HIPCHK(hipGetLastError());
-        }
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
+        // level k's dense list, then its shading (k_light reads only level k: on the side stream
+        // it starts as soon as the list exists and runs beside the next reflections)
+        auto level_lists = [&](int k) -> int {
+            hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k);
+            HIPCHK(hipGetLastError());
+            if (overlap) {
+                HIPCHK(hipEventRecord(p->ev_level[k], st));
+                HIPCHK(hipStreamWaitEvent(ls(k), p->ev_level[k], 0));
+            }
+            hipLaunchKernelGGL((k_light<PREC, GENPOW>), dim3(sblocks), dim3(BLOCK), 0, ls(k), p->hdr, p->d_tab,
+                               p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k));
+            HIPCHK(hipGetLastError());
+            return RT_OK;
+        };
+        if (nshade > 0 && (rc = level_lists(0)) != RT_OK) return rc;
         for (int k = 1; k <= nrefl; ++k) {
             if (lv)
                 hipLaunchKernelGGL((k_reflect<true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
-                                   k, ntiles, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+                                   k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
             else
                 hipLaunchKernelGGL((k_reflect<false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
-                                   k, ntiles, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+                                   k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
             HIPCHK(hipGetLastError());
-            hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k);
-            HIPCHK(hipGetLastError());
+            if ((rc = level_lists(k)) != RT_OK) return rc;
         }
-        for (int k = nshade - 1; k >= 0; --k) {
-            hipLaunchKernelGGL((k_shade<PREC, GENPOW>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                               p->d_itab, k, ntiles, o, qk(k), ik(k), nitems + k, p->d_colbuf);
+        if (overlap) { // join: reshading reads every level's colours and shadow answers
+            for (int x = 0; x < 2; ++x) {
+                HIPCHK(hipEventRecord(p->ev_join[x], p->side[x]));
+                HIPCHK(hipStreamWaitEvent(st, p->ev_join[x], 0));
+            }
+        }
+        for (int k = nrefl - 1; k >= 0; --k) {
+            if (p->hdr.n_light <= 32) // the shadow answers fit the record
+                hipLaunchKernelGGL((k_back<PREC, GENPOW, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                                   p->d_itab, k, o, qk(k), qk(k + 1), ik(k + 1), nitems + (k + 1), colk(k + 1), colk(k));
+            else
+                hipLaunchKernelGGL((k_back<PREC, GENPOW, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                                   p->d_itab, k, o, qk(k), qk(k + 1), ik(k + 1), nitems + (k + 1), colk(k + 1), colk(k));
             HIPCHK(hipGetLastError());
         }
     }
+    return RT_OK;
+}
+
+// RT_GRAPH=1 enables frame graphs.  Off by default: measured on MI355X (ROCm 7), replaying
+// the captured frame ran its kernels slower than direct launches (S64 4096^2: 1.35 vs 0.94
+// ms), the side stream's low priority does not survive capture.
+bool graphs_on() {
+    static bool on = [] {
+        const char *s = std::getenv("RT_GRAPH");
+        return s && std::strcmp(s, "1") == 0;
+    }();
+    return on;
+}
+
+// Run enqueue(stream) for a frame: directly, or through the cached graph of identical frames.
+template <typename F>
+int launch_frame(rt_prepared *p, const long long (&args)[12], hipStream_t st, F &&enqueue) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (!graphs_on() || hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+        return enqueue(st); // the caller is capturing (or graphs are off): plain launches
+    long long key[12];
+    std::memcpy(key, args, sizeof(key));
+    key[11] = (long long)p->gen; // a reallocated work space invalidates captured pointers
+    auto same = [&](const long long (&a)[12]) { return std::memcmp(a, key, sizeof(key)) == 0; };
+    if (p->gexec && same(p->gkey)) {
+        HIPCHK(hipGraphLaunch(p->gexec, st));
+        return RT_OK;
+    }
+    if (!(p->last_valid && same(p->last_key))) { // first time with these arguments: run directly
+        const int rc = enqueue(st);
+        std::memcpy(p->last_key, key, sizeof(key));
+        p->last_key[11] = (long long)p->gen;
+        p->last_valid = rc == RT_OK;
+        return rc;
+    }
+    // second identical frame (work space already sized): capture it on an internal stream
+    if (!p->cap) HIPCHK(hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking));
+    HIPCHK(hipStreamBeginCapture(p->cap, hipStreamCaptureModeRelaxed));
+    const int rc = enqueue(p->cap);
+    hipGraph_t gr = nullptr;
+    const hipError_t e = hipStreamEndCapture(p->cap, &gr);
+    if (rc != RT_OK || e != hipSuccess || (long long)p->gen != key[11]) {
+        if (gr) (void)hipGraphDestroy(gr);
+        p->last_valid = false;
+        return rc != RT_OK ? rc : RT_EHIP;
+    }
+    if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
+    p->gexec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&p->gexec, gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+    if (ei != hipSuccess) {
+        p->gexec = nullptr;
+        return RT_EHIP;
+    }
+    std::memcpy(p->gkey, key, sizeof(key));
+    HIPCHK(hipGraphLaunch(p->gexec, st));
     return RT_OK;
 }
 
@@ -1070,13 +1201,17 @@ int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, u
     int W = (int)width, H = (int)height, D = (int)depth, rb = (int)row_block, sh = (int)shard, ns = (int)nshards;
     const int slab_rows = (int)slab;
     if (!use_mega_engine()) { // the wavefront engine always evaluates the reference's exact order
-        if (precision == RT_OUT_F64)
+        const long long key[12] = {W, H, D, rb, sh, ns, precision, slab_rows, (long long)(intptr_t)d_out,
+                                   (long long)(intptr_t)d_levels, 0, 0};
+        return launch_frame(p, key, st, [&](hipStream_t s) {
+            if (precision == RT_OUT_F64)
+                return p->hdr.int_pow
+                           ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, s)
+                           : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, s);
             return p->hdr.int_pow
-                       ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)
-                       : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st);
-        return p->hdr.int_pow
-                   ? launch_wavefront<RT_OUT_F32, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)
-                   : launch_wavefront<RT_OUT_F32, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st);
+                       ? launch_wavefront<RT_OUT_F32, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, s)
+                       : launch_wavefront<RT_OUT_F32, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, s);
+        });
     }
 #define RT_DISPATCH(O, P)                                                                                          \
     return p->hdr.int_pow ? launch_t<O, P, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)           \

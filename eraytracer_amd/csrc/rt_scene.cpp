@@ -265,14 +265,20 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
     for (int i : tri) it.push_back(compact[i]);
     h.i_pl_id = (int)it.size();
     for (int i : pl) it.push_back(compact[i]);
+    while (it.size() % 4) it.push_back(0); // 16-byte rows
     h.i_obj_meta = (int)it.size();
     for (int i : objs) {
         int kind = e[i].kind == RT_SPHERE ? K_SPHERE : (e[i].kind == RT_TRIANGLE ? K_TRIANGLE : K_PLANE);
-        int local = 0;
         const std::vector<int> &grp = kind == K_SPHERE ? sph : (kind == K_TRIANGLE ? tri : pl);
-        for (size_t q = 0; q < grp.size(); q++)
+        // the canonical (first exactly equal) element is a record of the same type: its index
+        // within the type is stored here too, so a shadow target resolves in one load
+        const int r = root(e, i);
+        int local = 0, rlocal = 0;
+        for (size_t q = 0; q < grp.size(); q++) {
             if (grp[q] == i) local = (int)q;
-        it.insert(it.end(), {kind, local, compact[root(e, i)], 0});
+            if (grp[q] == r) rlocal = (int)q;
+        }
+        it.insert(it.end(), {kind, local, compact[r], rlocal});
     }
     // Occluder masks, per (light, target sphere).  Shadow rays to a target sphere t start at the
     // light L and point into the cone from L around ball(c_t, r_t); the target's own t* (its

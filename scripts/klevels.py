@@ -18,3 +18,16 @@ print(f"frames={fr['frames']} kernels/frame={fr['kernels_per_frame']} busy={fr['
       f"span={fr['avg_span_ns'] / 1e3:.1f} us")
 for lab, e in sorted(k.items(), key=lambda kv: (kv[0].split('#')[0], int(kv[0].split('#')[1]))):
     print(f"  {lab:12s} {e['avg_ns'] / 1e3:8.1f} us")
+
+if len(sys.argv) > 2 and sys.argv[2] == "--timeline":
+    import csv
+    from pmc_summary import frames
+    rows = []
+    with open(glob.glob(os.path.join(d, "trace", "*kernel_trace.csv"))[0]) as fh:
+        for r in csv.DictReader(fh):
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))))
+    rows.sort()
+    f = frames(rows)[-1]
+    t0 = min(s for _, (s, e) in f)
+    for lab, (s, e) in sorted(f, key=lambda x: x[1][0]):
+        print(f"  {lab:12s} {(s - t0) / 1e3:8.1f} -> {(e - t0) / 1e3:8.1f} us  ({(e - s) / 1e3:6.1f})")

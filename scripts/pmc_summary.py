@@ -96,7 +96,7 @@ def load_trace(d):
     if not fr:
         return None, None
     busy = [sum(e - s for _, (s, e, _) in f) for f in fr]
-    span = [f[-1][1][1] - f[0][1][0] for f in fr]
+    span = [max(e for _, (s, e, _) in f) - min(s for _, (s, e, _) in f) for f in fr]  # streams may overlap
     per = defaultdict(list)
     vg = {}
     for f in fr:

@@ -154,3 +154,35 @@ def test_fused_engine_parity():
     env = dict(os.environ, RT_ENGINE="fused", PYTHONPATH=root)
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "fused ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_repeated_launch_graph_replay(oracle):
+    """Identical rt_launch calls go direct, then captured, then replayed from a graph; a larger
+    frame in between reallocates the work space, which must invalidate the captured graph."""
+    import torch
+    L = N.lib()
+    scene = scenes.s64()
+    el = N.marshal(scene)
+    p = ctypes.c_void_p()
+    N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(p)), "rt_prepare")
+    try:
+        st = torch.cuda.current_stream().cuda_stream
+        w, h, d = 96, 80, 5
+        out = torch.empty((h, w, 3), dtype=torch.float64, device="cuda")
+        big = torch.empty((400, 320, 3), dtype=torch.float64, device="cuda")
+        imgs = []
+        for i in range(7):
+            out.fill_(-1.0)
+            if i == 3:  # a bigger frame grows every work buffer
+                N.check(L.rt_launch(p, 320, 400, d, 16, 0, 1, N.RT_OUT_F64, N.RT_ORDER_EXACT, big.data_ptr(), None, st))
+            N.check(L.rt_launch(p, w, h, d, 16, 0, 1, N.RT_OUT_F64, N.RT_ORDER_EXACT, out.data_ptr(), None, st))
+            torch.cuda.synchronize()
+            imgs.append(out.cpu().numpy().copy())
+        for i, im in enumerate(imgs[1:], 1):
+            assert np.array_equal(im, imgs[0]), f"launch {i} differs"
+        ref, _ = _oracle(oracle, scene, w, h, d)
+        _check(imgs[-1], ref)
+        refb, _ = _oracle(oracle, scene, 320, 400, d)
+        _check(big.cpu().numpy(), refb)
+    finally:
+        L.rt_release(p)
