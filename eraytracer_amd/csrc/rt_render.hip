@@ -1171,13 +1171,26 @@ int launch_frame(rt_prepared *p, const long long (&args)[12], hipStream_t st, F 
     return RT_OK;
 }
 
-// Engine: the wavefront pipeline (default) or the single fused kernel (RT_ENGINE=fused).
-bool use_mega_engine() {
-    static bool mega = [] {
+// Engine.  Small scenes are bound by per-level latency (every level of the wavefront pipeline
+// costs its kernels' fixed ramp-up) and run fastest as the single fused kernel; larger ones by
+// the scans, where the wavefront pipeline's coherent waves and overlap win.  Measured on
+// MI355X at 4096^2 depth 5: fused ahead up to 32 spheres (S4 74 vs 56 Gpx/s, S32 34.7 vs
+// 33.0), wavefront ahead from 48 (S48 21.6 vs 20.7, S64 18.6 vs 15.6, S256 d8 4.2 vs 1.7).
+// RT_ENGINE=fused | wave forces one; RT_FUSED_MAX_OBJECTS moves the crossover.
+constexpr int FUSED_MAX_OBJECTS = 40;
+bool use_mega_engine(const rt_prepared *p) {
+    static const int mode = [] { // 0 auto, 1 fused, 2 wave
         const char *s = std::getenv("RT_ENGINE");
-        return s && (std::strcmp(s, "fused") == 0 || std::strcmp(s, "mega") == 0);
+        if (s && (std::strcmp(s, "fused") == 0 || std::strcmp(s, "mega") == 0)) return 1;
+        if (s && std::strcmp(s, "wave") == 0) return 2;
+        return 0;
     }();
-    return mega;
+    static const int max_obj = [] {
+        const char *s = std::getenv("RT_FUSED_MAX_OBJECTS");
+        return s ? std::atoi(s) : FUSED_MAX_OBJECTS;
+    }();
+    if (mode) return mode == 1;
+    return p->hdr.n_obj <= max_obj;
 }
 
 } // namespace
@@ -1200,7 +1213,7 @@ int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, u
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     int W = (int)width, H = (int)height, D = (int)depth, rb = (int)row_block, sh = (int)shard, ns = (int)nshards;
     const int slab_rows = (int)slab;
-    if (!use_mega_engine()) { // the wavefront engine always evaluates the reference's exact order
+    if (!use_mega_engine(p)) { // the wavefront engine always evaluates the reference's exact order
         const long long key[12] = {W, H, D, rb, sh, ns, precision, slab_rows, (long long)(intptr_t)d_out,
                                    (long long)(intptr_t)d_levels, 0, 0};
         return launch_frame(p, key, st, [&](hipStream_t s) {

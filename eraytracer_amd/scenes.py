@@ -94,7 +94,10 @@ def s256():
 def named(name: str):
     from .records import scene as default_scene
     table = {"default": default_scene, "s64": s64, "s256": s256}
-    try:
-        return table[name.lower()]()
-    except KeyError:
-        raise ValueError(f"unknown scene {name!r}; expected one of {sorted(table)}") from None
+    key = name.lower()
+    if key in table:
+        return table[key]()
+    if key.startswith("s") and key[1:].isdigit() and 1 <= int(key[1:]) <= 4000:
+        n = int(key[1:])  # sN: N spheres, seed 0x5EED<N as four decimal digits> like S64 / S256
+        return synthetic_scene(n, int(f"5EED{n:04d}", 16))
+    raise ValueError(f"unknown scene {name!r}; expected one of {sorted(table)} or sN")

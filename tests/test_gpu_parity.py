@@ -129,9 +129,11 @@ def test_full_size_sampled_rows(oracle):
     assert lv.max() <= 5
 
 
-def test_fused_engine_parity():
-    """The alternative single-kernel engine (RT_ENGINE=fused, chosen once per process) on the
-    same parity cases, run in a child process."""
+@pytest.mark.parametrize("engine", ["fused", "wave"])
+def test_forced_engine_parity(engine):
+    """Each engine forced for every scene (RT_ENGINE, read once per process, so in a child
+    process): by default small scenes take the fused kernel and large ones the wavefront
+    pipeline, and both must keep the reference's answers on every case."""
     import os
     import subprocess
     import sys
@@ -143,17 +145,19 @@ def test_fused_engine_parity():
         "from tests.test_oracle import TRICKY\n"
         "cases = [(scenes.named(n), w, h, d) for n, w, h, d in [('default', 64, 48, 5), ('s64', 64, 64, 5),"
         " ('s256', 40, 32, 8)]] + [(mk(), 40, 30, 3) for mk in TRICKY]\n"
+        # more lights than the 32 shadow answers a record keeps: the reshading retests shadows
+        "cases.append((scenes.synthetic_scene(24, 0x5EED4040, n_lights=40), 48, 40, 4))\n"
         "for order in ('exact', 'fast'):\n"
         "    for sc, w, h, d in cases:\n"
         "        img, lv = render(w, h, sc, d, levels=True, order=order)\n"
         "        ref, rlv = O.render(N.marshal(sc), w, h, d, mode=O.MEMO, levels=True)\n"
         "        assert np.array_equal(lv, rlv)\n"
         "        assert np.abs(img - ref).max() <= 1e-5, (order, w, h, d)\n"
-        "print('fused ok')\n")
+        "print('engine ok')\n")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, RT_ENGINE="fused", PYTHONPATH=root)
+    env = dict(os.environ, RT_ENGINE=engine, PYTHONPATH=root)
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0 and "fused ok" in r.stdout, r.stdout + r.stderr
+    assert r.returncode == 0 and "engine ok" in r.stdout, r.stdout + r.stderr
 
 
 def test_repeated_launch_graph_replay(oracle):
