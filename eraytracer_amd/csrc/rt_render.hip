@@ -374,34 +374,10 @@ __device__ __forceinline__ void scan_spheres(const Scene &S, int org, const D3 &
 // Reflection rays are culled per group of lanes leaving the same object (at most
 // MAX_GROUPS beams, the last one covering every remaining lane): lanes on different objects
 // would otherwise share one wide beam.  Testing a sphere twice cannot change the nearest.
-constexpr int MAX_GROUPS = 3;
+// The triangles and planes of the scene, folded into the running nearest (bt, bid).
 template <bool PRE>
-__device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, bool act,
-                                       int grp = -1) {
+__device__ __forceinline__ void scan_tri_pl(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, int &bid) {
     const SceneHdr &h = S.h;
-    bt = __builtin_inf();
-    int bid = 0x7fffffff;
-    if (__ballot(act) == 0) return -1; // nothing to trace in this wave
-    const double A4 = 4 * (d.x * d.x + d.y * d.y + d.z * d.z);
-    RT_STAT(PRE ? ST_NEAR_PRE : ST_NEAR_GEN, 1);
-    RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
-    unsigned long long rem = __ballot(act);
-    for (int g = 0; g < MAX_GROUPS && rem; ++g) {
-        bool sel = act;
-        if (!PRE) {
-            const int gv = __builtin_amdgcn_readlane(grp, __builtin_ctzll(rem));
-            sel = (g == MAX_GROUPS - 1) ? ((rem >> (threadIdx.x & 63)) & 1) != 0 : (act && grp == gv);
-        }
-        rem = PRE ? 0ull : (rem & ~__ballot(sel));
-        const Beam b = make_beam(h, sel, o, d, PRE);
-        RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
-        for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
-            const unsigned long long m =
-                b.on ? cull_chunk(S, b, chunk, PRE ? org : -1) : chunk_all(h.n_sph, chunk);
-            scan_spheres<PRE>(S, org, o, d, A4, chunk, m, bt, bid);
-        }
-        if (!b.on) break; // everything was scanned
-    }
     for (int k = 0; k < h.n_tri; ++k) {
         const double *g = S.tab + h.o_tri + k * TRI_W;
         D3 e1 = {g[3], g[4], g[5]}, e2 = {g[6], g[7], g[8]};
@@ -430,7 +406,122 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
             if (nearer(t, id, bt, bid)) { bt = t; bid = id; }
         }
     }
+}
+
+constexpr int MAX_GROUPS = 3;
+template <bool PRE>
+__device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, bool act,
+                                       int grp = -1) {
+    const SceneHdr &h = S.h;
+    bt = __builtin_inf();
+    int bid = 0x7fffffff;
+    if (__ballot(act) == 0) return -1; // nothing to trace in this wave
+    const double A4 = 4 * (d.x * d.x + d.y * d.y + d.z * d.z);
+    RT_STAT(PRE ? ST_NEAR_PRE : ST_NEAR_GEN, 1);
+    RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
+    unsigned long long rem = __ballot(act);
+    for (int g = 0; g < MAX_GROUPS && rem; ++g) {
+        bool sel = act;
+        if (!PRE) {
+            const int gv = __builtin_amdgcn_readlane(grp, __builtin_ctzll(rem));
+            sel = (g == MAX_GROUPS - 1) ? ((rem >> (threadIdx.x & 63)) & 1) != 0 : (act && grp == gv);
+        }
+        rem = PRE ? 0ull : (rem & ~__ballot(sel));
+        const Beam b = make_beam(h, sel, o, d, PRE);
+        RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
+        for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
+            const unsigned long long m =
+                b.on ? cull_chunk(S, b, chunk, PRE ? org : -1) : chunk_all(h.n_sph, chunk);
+            scan_spheres<PRE>(S, org, o, d, A4, chunk, m, bt, bid);
+        }
+        if (!b.on) break; // everything was scanned
+    }
+    scan_tri_pl<PRE>(S, org, o, d, bt, bid);
     return (act && bid != 0x7fffffff) ? bid : -1;
+}
+
+// Beam of a wave holding two primary rays per lane (an 8x16 pixel block) from a tabled
+// origin: the same cone construction as make_beam, over both ray sets.
+__device__ __forceinline__ Beam make_beam_pair(const SceneHdr &h, bool a0, const D3 &d0, bool a1, const D3 &d1) {
+    Beam b;
+    b.on = false;
+    b.ax = b.ay = b.az = b.c = b.s = b.mx = b.my = b.mz = b.ro = 0.0;
+    const unsigned long long m0 = __ballot(a0), m1 = __ballot(a1);
+    if (!h.cull_ok || (m0 | m1) == 0) return b;
+    // axis: the ray of pixel (3, 7) of the block (set 0, lane 59), else the first active ray
+    double rx, ry, rz;
+    if ((m0 >> 59) & 1) {
+        rx = lane_f64(d0.x, 59); ry = lane_f64(d0.y, 59); rz = lane_f64(d0.z, 59);
+    } else if (m0) {
+        const int l = __builtin_ctzll(m0);
+        rx = lane_f64(d0.x, l); ry = lane_f64(d0.y, l); rz = lane_f64(d0.z, l);
+    } else {
+        const int l = __builtin_ctzll(m1);
+        rx = lane_f64(d1.x, l); ry = lane_f64(d1.y, l); rz = lane_f64(d1.z, l);
+    }
+    const double n2 = rx * rx + ry * ry + rz * rz;
+    if (!(n2 > 0.0)) return b;
+    const double inv = uniform(1.0 / sqrt(n2));
+    const double ax = rx * inv, ay = ry * inv, az = rz * inv;
+    constexpr double DIR_TOL = 1.0e-6; // as in make_beam
+    auto lane_terms = [&](bool a, const D3 &d, double &cl, double &q2) {
+        const double dd = d.x * d.x + d.y * d.y + d.z * d.z;
+        cl = ax * d.x + ay * d.y + az * d.z;
+        const double qx = ay * d.z - az * d.y, qy = az * d.x - ax * d.z, qz = ax * d.y - ay * d.x;
+        q2 = qx * qx + qy * qy + qz * qz;
+        return a && !(dd > 1.0 - DIR_TOL && dd < 1.0 + DIR_TOL);
+    };
+    double cl0, q20, cl1, q21;
+    const bool bad0 = lane_terms(a0, d0, cl0, q20); // both sets evaluated (no short circuit)
+    const bool bad1 = lane_terms(a1, d1, cl1, q21);
+    const bool bad = bad0 || bad1;
+    const double cmin = fmin(a0 ? cl0 : 2.0, a1 ? cl1 : 2.0);
+    const double q2max = fmax(a0 ? q20 : 0.0, a1 ? q21 : 0.0);
+    const double c = uniform(wave_min(cmin)) - CULL_EPS - 2 * DIR_TOL;
+    // sqrt is monotone and correctly rounded: sqrt(max q2) = max sqrt(q2)
+    const double s = uniform(sqrt(wave_max(q2max))) + CULL_EPS + 2 * DIR_TOL;
+    if (__ballot(bad) != 0 || !(c > 0.0)) return b;
+    b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
+    b.on = true;
+    return b;
+}
+
+// nearest_object_intersecting_ray/6 for two rays per lane from tabled origin `org` (primary
+// rays): one beam and one candidate walk serve both, and each candidate's two tests are
+// independent (instruction-level parallelism for the wave).
+__device__ __forceinline__ void nearest_pair(const Scene &S, int org, const D3 &o, const D3 &d0, const D3 &d1, bool a0,
+                                             bool a1, int &id0, double &t0, int &id1, double &t1) {
+    const SceneHdr &h = S.h;
+    double bt0 = __builtin_inf(), bt1 = __builtin_inf();
+    int bid0 = 0x7fffffff, bid1 = 0x7fffffff;
+    id0 = id1 = -1;
+    t0 = t1 = 0.0;
+    if (__ballot(a0 | a1) == 0) return;
+    const double A40 = 4 * (d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
+    const double A41 = 4 * (d1.x * d1.x + d1.y * d1.y + d1.z * d1.z);
+    const Beam b = make_beam_pair(h, a0, d0, a1, d1);
+    for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
+        unsigned long long m = b.on ? cull_chunk(S, b, chunk, org) : chunk_all(h.n_sph, chunk);
+        while (m) {
+            const int k = chunk + __builtin_ctzll(m);
+            m &= m - 1;
+            const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
+            const double qx = q[0], qy = q[1], qz = q[2], C = q[3];
+            const int id = S.itab[h.i_sph_id + k];
+            double u0, u1;
+            const bool h0 = sph_t_wave(2 * (d0.x * qx + d0.y * qy + d0.z * qz), C, A40, u0);
+            const bool h1 = sph_t_wave(2 * (d1.x * qx + d1.y * qy + d1.z * qz), C, A41, u1);
+            const bool up0 = h0 & nearer(u0, id, bt0, bid0), up1 = h1 & nearer(u1, id, bt1, bid1);
+            bt0 = up0 ? u0 : bt0; bid0 = up0 ? id : bid0;
+            bt1 = up1 ? u1 : bt1; bid1 = up1 ? id : bid1;
+        }
+    }
+    if (h.n_tri | h.n_pl) {
+        scan_tri_pl<true>(S, org, o, d0, bt0, bid0);
+        scan_tri_pl<true>(S, org, o, d1, bt1, bid1);
+    }
+    if (a0 && bid0 != 0x7fffffff) { id0 = bid0; t0 = bt0; }
+    if (a1 && bid1 != 0x7fffffff) { id1 = bid1; t1 = bt1; }
 }
 
 // Hit point and normal of object `id` at distance t (as computed inside the reference's
@@ -1064,10 +1155,10 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
         dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
         if (lv)
-            hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H, D,
+            hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H, D,
                                rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles);
         else
-            hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H,
+            hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H,
                                D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles);
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
