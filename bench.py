@@ -36,8 +36,8 @@ PEAK_HBM_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--scene", default="s64")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--depth", type=int, default=5)
@@ -76,9 +76,10 @@ def cpu_baseline(scene, W, H, depth, target_s):
                       f"reflection recursion), {threads} threads; BEAM (erl) is not installed on the box"}
 
 
-def traffic_from_profiles(workload_key):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary of the same workload
-    (profiles/*pmc*.json written by scripts/profile.sh), or None."""
+def profile_for(workload_key):
+    """The committed rocprofv3 summary of the same workload (profiles/*pmc*.json, written by
+    scripts/pmc_summary.py from scripts/profile.sh passes; the newest by name wins), or None.
+    Supplies the measured HBM bytes per frame launch and the executed FP64 issue fraction."""
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
@@ -86,7 +87,7 @@ def traffic_from_profiles(workload_key):
         except Exception:
             continue
         if d.get("workload") == workload_key and d.get("hbm_bytes_per_launch") is not None:
-            best = (d["hbm_bytes_per_launch"], os.path.relpath(p, ROOT))
+            best = (d, os.path.relpath(p, ROOT))
     return best
 
 
@@ -170,7 +171,9 @@ def main():
         valu_ach = ops_rank / k_s / 1e12
         hbm_ach = px_rank * bytes_px / k_s / 1e9
         wkey = f"{args.scene}-{W}x{H}-d{args.depth}-{args.order}-{args.precision}-n{world}"
-        tr = traffic_from_profiles(wkey)
+        prof = profile_for(wkey)
+        traffic = prof[0]["hbm_bytes_per_launch"] if prof else None
+        executed = prof[0].get("derived", {}).get("f64_issue_frac_of_peak_39.3T") if prof else None
         line = {
             "metric": "Mpixels/sec at 4096x4096, recursion depth 5 (frame rendered into HBM, gathered to rank 0)",
             "value": round(value, 3),
@@ -192,13 +195,17 @@ def main():
                        "lights": counts["lights"]},
             "roofline": {"bound": "valu", "achieved": round(valu_ach, 3), "peak": PEAK_FP64_VALU_TOPS,
                          "unit": "TFLOP/s", "frac": round(valu_ach / PEAK_FP64_VALU_TOPS, 4),
-                         "traffic": tr[0] if tr else None,
-                         "note": "FP64 VALU (binding): algorithmic binary64 ops per launch (SURVEY.md 8d weights, "
-                                 f"{ops_rank:.4g} ops for {px_rank} px) / mean render-launch time "
-                                 f"{kern_ms:.3f} ms; peak = 78.6 TFLOP/s FP64 vector / 2 (no FMA: contraction off)"
-                                 + (f"; traffic from {tr[1]}" if tr else "")},
+                         "traffic": traffic,
+                         "executed_f64_frac": round(executed, 4) if executed is not None else None,
+                         "note": "FP64 VALU (binding): algorithmic binary64 ops per frame launch as SURVEY.md 8d "
+                                 f"counts them for the reference's brute-force scans ({ops_rank:.4g} ops for "
+                                 f"{px_rank} px) / mean launch time {kern_ms:.3f} ms (HIP events on the launch "
+                                 "stream); peak = 78.6 TFLOP/s FP64 vector / 2 (no FMA: contraction off). frac > 1 "
+                                 "means the beam/occluder culling skips reference work; executed_f64_frac is the "
+                                 "FP64 instructions actually issued (rocprofv3 PMC, x64 lanes) / frame span / peak"
+                                 + (f"; traffic and executed from {prof[1]}" if prof else "")},
             "roofline_hbm": {"bound": "hbm", "achieved": round(hbm_ach, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": round(hbm_ach / PEAK_HBM_GBS, 6), "traffic": tr[0] if tr else None},
+                             "frac": round(hbm_ach / PEAK_HBM_GBS, 6), "traffic": traffic},
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_max_rank": round(kern_ms_max, 4),
             "kernel_mpx_s": round(px_rank / k_s / 1e6, 3),

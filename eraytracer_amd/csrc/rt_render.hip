@@ -902,9 +902,13 @@ struct rt_prepared {
     int *d_items = nullptr;   // per-level record counts, then per-level dense slot lists
     size_t items_bytes = 0;
     // the shadow pass runs on a second, low-priority stream beside the reflection chain
-    hipStream_t side[2] = {};  // level 0's shading; the deeper levels' shading
-    hipEvent_t ev_level[RT_MAX_DEPTH + 1] = {};
-    hipEvent_t ev_join[2] = {};
+    // shading of level 0 and of the deeper levels.  The caller's stream plus these stay
+    // within the hardware queues a process gets by default (GPU_MAX_HW_QUEUES=4): streams
+    // sharing a queue block each other behind their event waits (measured: 5 streams, S64
+    // 11 Gpx/s; 3 side streams were no faster than 2 — the chip is saturated in the overlap)
+    hipStream_t side[2] = {};
+    hipEvent_t ev_level[RT_MAX_DEPTH + 1] = {}; // level k's list is ready
+    hipEvent_t ev_lit[RT_MAX_DEPTH + 1] = {};   // level k is shaded
     // Frames repeat with identical arguments (bench, multi-GPU renderer): the second identical
     // rt_launch captures the frame's launch sequence into a graph, later ones replay it.
     // gen counts work-space reallocations, which invalidate captured pointers.
@@ -1049,7 +1053,7 @@ int rt_release(rt_prepared *p) {
     if (p->d_items) (void)hipFree(p->d_items);
     for (hipEvent_t &e : p->ev_level)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t &e : p->ev_join)
+    for (hipEvent_t &e : p->ev_lit)
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t &x : p->side)
         if (x) (void)hipStreamDestroy(x);
@@ -1089,7 +1093,7 @@ int side_stream(rt_prepared *p) {
     HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     for (hipStream_t &x : p->side) HIPCHK(hipStreamCreateWithPriority(&x, hipStreamNonBlocking, least));
     for (hipEvent_t &e : p->ev_level) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (hipEvent_t &e : p->ev_join) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t &e : p->ev_lit) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return RT_OK;
 }
 
@@ -1133,8 +1137,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     if (rc == RT_OK && overlap) rc = side_stream(p);
     if (rc != RT_OK) return rc;
     // streams of the shading pass: level 0 (the bulk) beside the whole reflection chain, the
-    // deeper levels on a second stream so they need not wait for level 0's shading
-    auto ls = [&](int k) { return overlap ? p->side[k > 0 ? 1 : 0] : st; };
+    // next levels each on their own, so no level waits for another's shading
+    auto ls = [&](int k) { return overlap ? p->side[std::min(k, 1)] : st; };
     HitRec *q = static_cast<HitRec *>(p->d_queue);
     const int nrefl = (p->hdr.n_light > 0 && D > 1) ? D - 1 : 0;
     const int nshade = D > 0 ? 1 + nrefl : 0;
@@ -1174,6 +1178,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             hipLaunchKernelGGL((k_light<PREC, GENPOW>), dim3(sblocks), dim3(BLOCK), 0, ls(k), p->hdr, p->d_tab,
                                p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k));
             HIPCHK(hipGetLastError());
+            if (overlap) HIPCHK(hipEventRecord(p->ev_lit[k], ls(k)));
             return RT_OK;
         };
         if (nshade > 0 && (rc = level_lists(0)) != RT_OK) return rc;
@@ -1187,13 +1192,12 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             HIPCHK(hipGetLastError());
             if ((rc = level_lists(k)) != RT_OK) return rc;
         }
-        if (overlap) { // join: reshading reads every level's colours and shadow answers
-            for (int x = 0; x < 2; ++x) {
-                HIPCHK(hipEventRecord(p->ev_join[x], p->side[x]));
-                HIPCHK(hipStreamWaitEvent(st, p->ev_join[x], 0));
-            }
-        }
+        // reshading level k reads level k+1's final colours and level k's shadow answers: it
+        // waits for those two levels' shading only (level 0's, the longest, joins last)
+        if (overlap && nrefl > 0) HIPCHK(hipStreamWaitEvent(st, p->ev_lit[nrefl], 0));
+        if (overlap && nrefl == 0 && nshade > 0) HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
         for (int k = nrefl - 1; k >= 0; --k) {
+            if (overlap) HIPCHK(hipStreamWaitEvent(st, p->ev_lit[k], 0));
             if (p->hdr.n_light <= 32) // the shadow answers fit the record
                 hipLaunchKernelGGL((k_back<PREC, GENPOW, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
                                    p->d_itab, k, o, qk(k), qk(k + 1), ik(k + 1), nitems + (k + 1), colk(k + 1), colk(k));

@@ -141,7 +141,8 @@ def main():
     tr, tr_k = load_trace(src)
     out = {"workload": key, "source": os.path.basename(src.rstrip("/")), "unit": "one frame launch",
            "trace": tr, "counters": pmc, "frames_per_counter": nfr,
-           "derived": derive(pmc, tr["avg_busy_ns"] if tr else None), "kernels": {}}
+           # frame-level rates over the frame's wall span (the engine's streams overlap)
+           "derived": derive(pmc, tr["avg_span_ns"] if tr else None), "kernels": {}}
     for lab in sorted(set(pmc_k) | set(tr_k or {}), key=lambda s: (s.split("#")[0], int(s.split("#")[1]))):
         ent = dict((tr_k or {}).get(lab, {}))
         ent["counters"] = pmc_k.get(lab, {})
