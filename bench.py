@@ -44,36 +44,44 @@ def parse():
     ap.add_argument("--order", default="exact", choices=["exact", "fast"])
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--row-block", type=int, default=16)
+    ap.add_argument("--spp", type=int, default=1, help="samples per pixel (RT_SUPERSAMPLING; BASELINE config 5: 16)")
+    ap.add_argument("--seed", type=int, default=0x5EED0005)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-boundary", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(scene, W, H, depth, target_s):
+def cpu_baseline(scene, W, H, depth, target_s, spp=1, seed=0):
     """The C oracle in the reference's literal recursion (lighting_function recomputes the
     reflection per light, raytracer.erl:211-224), threaded over the box's CPU share, on a
-    bounded sample of rows spread over the same frame."""
+    bounded sample of rows spread over the same frame.  The literal recursion is exponential
+    in depth (L^(depth-1) re-evaluations), so deeper or supersampled configs use the
+    memoised oracle (same results) and say so."""
     from eraytracer_amd import _native as N
     from oracle import oracle as O
     O.build()
     el = N.marshal(scene)
     threads = min(16, os.cpu_count() or 1)
+    literal = spp == 1 and depth <= 5
+    mode = O.LITERAL if literal else O.MEMO
     # calibrate on one row, then take evenly spaced rows to fill ~target_s seconds
     t0 = time.perf_counter()
-    O.render(el, W, H, depth, mode=O.LITERAL, threads=threads, row0=H // 2, nrows=1)
+    O.render(el, W, H, depth, mode=mode, threads=threads, row0=H // 2, nrows=1, spp=spp, seed=seed)
     per_row = max(time.perf_counter() - t0, 1e-4)
     nrows = int(max(1, min(H, target_s / per_row)))
     rows = sorted(set(int(r) for r in [(i * H) // nrows + (H // nrows) // 2 for i in range(nrows)]))
     t0 = time.perf_counter()
     for r in rows:
-        O.render(el, W, H, depth, mode=O.LITERAL, threads=threads, row0=r, nrows=1)
+        O.render(el, W, H, depth, mode=mode, threads=threads, row0=r, nrows=1, spp=spp, seed=seed)
     dt = time.perf_counter() - t0
     px = len(rows) * W
+    how = ("ORC_LITERAL (the reference's per-light reflection recursion)" if literal else
+           "ORC_MEMO (reflection once per hit; the literal recursion is exponential in depth)")
     return {"value": px / dt / 1e6, "unit": "Mpixels/s", "cores": threads, "kind": "port",
-            "sample": f"{len(rows)} evenly spaced rows x {W} px of the same {W}x{H} depth-{depth} frame "
-                      f"({px} px, {dt:.1f} s), oracle/rt_oracle.c ORC_LITERAL (the reference's per-light "
-                      f"reflection recursion), {threads} threads; BEAM (erl) is not installed on the box"}
+            "sample": f"{len(rows)} evenly spaced rows x {W} px of the same {W}x{H} depth-{depth}"
+                      + (f" x{spp} spp" if spp > 1 else "") + f" frame ({px} px, {dt:.1f} s), oracle/rt_oracle.c "
+                      f"{how}, {threads} threads; BEAM (erl) is not installed on the box"}
 
 
 def profile_for(workload_key):
@@ -108,13 +116,17 @@ def main():
             sys.exit("bench.py: --gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     torch.cuda.set_device(local)
     if world > 1:
+        # RCCL brings its own stream(s); with torch's and the library's two shading side streams
+        # a rank would exceed the 4 hardware queues a process gets, and streams sharing a queue
+        # stall behind each other's event waits.  The gather dominates at N > 1 anyway.
+        os.environ.setdefault("RT_LIT_STREAM", "0")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     W = H = args.size
     scene = scenes.named(args.scene)
     counts = workload.scene_counts(scene)
     fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
-                       precision=args.precision, order=args.order)
+                       precision=args.precision, order=args.order, spp=args.spp, seed=args.seed)
 
     # untimed: work count of this rank's rows (levels of every pixel's reflection chain)
     lv_fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
@@ -126,7 +138,8 @@ def main():
     hist = torch.bincount(lv_fr.levels[valid].flatten().to(torch.int64), minlength=args.depth + 1).cpu().numpy()
     lv_fr.close()
     del lv_fr
-    ops_rank = workload.ops_from_levels(hist, args.depth, counts)
+    # with spp > 1 the work is estimated as spp times that of the unjittered frame
+    ops_rank = workload.ops_from_levels(hist, args.depth, counts) * args.spp
     px_rank = int(hist.sum())
 
     for _ in range(args.warmup):
@@ -170,7 +183,8 @@ def main():
         k_s = kern_ms / 1e3
         valu_ach = ops_rank / k_s / 1e12
         hbm_ach = px_rank * bytes_px / k_s / 1e9
-        wkey = f"{args.scene}-{W}x{H}-d{args.depth}-{args.order}-{args.precision}-n{world}"
+        wkey = f"{args.scene}-{W}x{H}-d{args.depth}-{args.order}-{args.precision}-n{world}" + (
+            f"-spp{args.spp}" if args.spp > 1 else "")
         prof = profile_for(wkey)
         traffic = prof[0]["hbm_bytes_per_launch"] if prof else None
         executed = prof[0].get("derived", {}).get("f64_issue_frac_of_peak_39.3T") if prof else None
@@ -187,7 +201,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"{args.scene.upper()} {W}x{H} depth {args.depth}", "scene": args.scene,
+            "config": {"workload": f"{args.scene.upper()} {W}x{H} depth {args.depth}"
+                       + (f" x{args.spp} spp" if args.spp > 1 else ""), "scene": args.scene, "spp": args.spp,
                        "width": W, "height": H, "depth": args.depth, "order": args.order,
                        "framebuffer": args.precision, "row_block": args.row_block,
                        "parallelism": f"rows{world}" + ("+rccl_gather" if world > 1 else ""),
@@ -214,15 +229,17 @@ def main():
         if world == 1 and not args.no_boundary:
             from eraytracer_amd.raytracer import render
             st = {}
-            render(W, H, scene, args.depth, precision=args.precision, order=args.order, stats=st)
+            render(W, H, scene, args.depth, precision=args.precision, order=args.order, stats=st, spp=args.spp,
+                   seed=args.seed)
             ts = []
             for _ in range(2):
                 st = {}
-                render(W, H, scene, args.depth, precision=args.precision, order=args.order, stats=st)
+                render(W, H, scene, args.depth, precision=args.precision, order=args.order, stats=st, spp=args.spp,
+                       seed=args.seed)
                 ts.append(st["total_ms"])
             line["boundary_mpx_s"] = round(frame_px / (min(ts) / 1e3) / 1e6, 3)
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(scene, W, H, args.depth, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(scene, W, H, args.depth, args.cpu_seconds, args.spp, args.seed)
         print(json.dumps(line), flush=True)
     fr.close()
     if world > 1:

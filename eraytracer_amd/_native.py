@@ -28,7 +28,7 @@ RT_MAX_DEPTH = 16
 # every symbol include/rt_mi355x.h declares (tests/test_boundary.py checks the export list)
 EXPORTS = (
     "rt_abi_version", "rt_strerror", "rt_device_count", "rt_scene_check", "rt_scene_canon",
-    "rt_render", "rt_prepare", "rt_shard_rows", "rt_launch", "rt_unshard", "rt_release",
+    "rt_render", "rt_prepare", "rt_shard_rows", "rt_launch", "rt_launch_spp", "rt_unshard", "rt_release",
 )
 
 
@@ -74,7 +74,8 @@ class RtElem(ctypes.Structure):
 class RtOpts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("first_dev", ctypes.c_int32), ("ndev", ctypes.c_int32),
                 ("precision", ctypes.c_int32), ("order", ctypes.c_int32), ("row_block", ctypes.c_uint32),
-                ("out_levels", ctypes.c_void_p)]
+                ("out_levels", ctypes.c_void_p), ("spp", ctypes.c_uint32), ("reserved0", ctypes.c_uint32),
+                ("seed", ctypes.c_uint64)]
 
 
 class RtStats(ctypes.Structure):
@@ -120,6 +121,7 @@ def lib() -> ctypes.CDLL:
     L.rt_shard_rows.restype = u32
     L.rt_shard_rows.argtypes = [u32, u32, u32]
     L.rt_launch.argtypes = [vp, u32, u32, u32, u32, u32, u32, i32, i32, vp, vp, vp]
+    L.rt_launch_spp.argtypes = [vp, u32, u32, u32, u32, u32, u32, i32, i32, u32, ctypes.c_uint64, vp, vp, vp]
     L.rt_unshard.argtypes = [vp, u32, u32, u32, u32, i32, vp, vp]
     L.rt_release.argtypes = [vp]
     _LIB = L

@@ -28,6 +28,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -896,6 +897,8 @@ struct rt_prepared {
     void *d_queue = nullptr;  // HitRec[slab pixels * depth]
     size_t queue_bytes = 0;
     double *d_colbuf = nullptr; // colours of levels 1 .. depth-1, 3 doubles per slot
+    double *d_sample = nullptr; // supersampling: one sample's slab and the running sum
+    size_t sample_bytes = 0;
     size_t colbuf_bytes = 0;
     int *d_counts = nullptr;  // per level and tile: queue lengths
     size_t counts_bytes = 0;
@@ -1049,6 +1052,7 @@ int rt_release(rt_prepared *p) {
     (void)hipFree(p->d_itab);
     if (p->d_queue) (void)hipFree(p->d_queue);
     if (p->d_colbuf) (void)hipFree(p->d_colbuf);
+    if (p->d_sample) (void)hipFree(p->d_sample);
     if (p->d_counts) (void)hipFree(p->d_counts);
     if (p->d_items) (void)hipFree(p->d_items);
     for (hipEvent_t &e : p->ev_level)
@@ -1113,7 +1117,7 @@ int grow(void **buf, size_t *have, size_t need, unsigned *gen) {
 
 template <int PREC, bool GENPOW>
 int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns, int slab_rows, void *out,
-                     uint8_t *levels, hipStream_t st) {
+                     uint8_t *levels, hipStream_t st, int spp = 1, int sample = 0, unsigned long long seed = 0) {
     const int nlev = D > 0 ? D : 1;
     const size_t per_row = (size_t)W * nlev * sizeof(HitRec);
     int pass_rows = (int)std::min<size_t>((size_t)slab_rows, std::max<size_t>(TILE, queue_budget() / per_row));
@@ -1160,10 +1164,10 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
         if (lv)
             hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H, D,
-                               rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles);
+                               rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed);
         else
             hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H,
-                               D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles);
+                               D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed);
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
         // level k's dense list, then its shading (k_light reads only level k: on the side stream
@@ -1294,6 +1298,13 @@ extern "C" {
 
 int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, uint32_t row_block, uint32_t shard,
               uint32_t nshards, int precision, int order, void *d_out, uint8_t *d_levels, void *stream) {
+    return rt_launch_spp(p, width, height, depth, row_block, shard, nshards, precision, order, 1, 0, d_out, d_levels,
+                         stream);
+}
+
+int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, uint32_t row_block,
+                  uint32_t shard, uint32_t nshards, int precision, int order, uint32_t spp, uint64_t seed,
+                  void *d_out, uint8_t *d_levels, void *stream) {
     if (!p || !d_out) return RT_EBADARG;
     if (width == 0 && height == 0) return RT_DONE;
     if (width == 0 || height == 0) return RT_EBADARG;
@@ -1301,6 +1312,8 @@ int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, u
     if (row_block == 0 || nshards == 0 || shard >= nshards) return RT_EBADARG;
     if (precision != RT_OUT_F64 && precision != RT_OUT_F32) return RT_EBADARG;
     if (order != RT_ORDER_EXACT && order != RT_ORDER_FAST) return RT_EBADARG;
+    if (spp == 0) return RT_EBADARG;
+    if (spp > RT_MAX_SPP) return RT_ETOOBIG;
     if (width > (1u << 20) || height > (1u << 20)) return RT_ETOOBIG;
     uint32_t slab = rt_shard_rows(height, row_block, nshards);
     if ((uint64_t)slab > 65535ull * TILE) return RT_ETOOBIG;
@@ -1308,6 +1321,26 @@ int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, u
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     int W = (int)width, H = (int)height, D = (int)depth, rb = (int)row_block, sh = (int)shard, ns = (int)nshards;
     const int slab_rows = (int)slab;
+    if (spp > 1) { // RT_SUPERSAMPLING, on the wavefront engine: one pass per sample, summed in order
+        const size_t n = (size_t)slab_rows * W * 3;
+        int rc = grow(reinterpret_cast<void **>(&p->d_sample), &p->sample_bytes, 2 * n * sizeof(double), &p->gen);
+        if (rc != RT_OK) return rc;
+        double *smp = p->d_sample, *acc = p->d_sample + n;
+        const int blocks = (int)std::min<size_t>(8192, (n + 255) / 256);
+        for (int s = 0; s < (int)spp; ++s) {
+            rc = p->hdr.int_pow ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, slab_rows, smp,
+                                                                      s == 0 ? d_levels : nullptr, st, (int)spp, s, seed)
+                                : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, slab_rows, smp,
+                                                                     s == 0 ? d_levels : nullptr, st, (int)spp, s, seed);
+            if (rc != RT_OK) return rc;
+            if (precision == RT_OUT_F64)
+                hipLaunchKernelGGL(k_accum<RT_OUT_F64>, dim3(blocks), dim3(256), 0, st, n, smp, acc, d_out, s, (int)spp);
+            else
+                hipLaunchKernelGGL(k_accum<RT_OUT_F32>, dim3(blocks), dim3(256), 0, st, n, smp, acc, d_out, s, (int)spp);
+            HIPCHK(hipGetLastError());
+        }
+        return RT_OK;
+    }
     if (!use_mega_engine(p)) { // the wavefront engine always evaluates the reference's exact order
         const long long key[12] = {W, H, D, rb, sh, ns, precision, slab_rows, (long long)(intptr_t)d_out,
                                    (long long)(intptr_t)d_levels, 0, 0};
@@ -1377,10 +1410,12 @@ int rt_render(const rt_elem *scene, uint32_t n, uint32_t width, uint32_t height,
     std::memset(&o, 0, sizeof(o));
     o.ndev = 1;
     o.row_block = 16;
+    o.spp = 1;
     if (opts && opts->struct_size) {
         std::memcpy(&o, opts, opts->struct_size < sizeof(o) ? opts->struct_size : sizeof(o));
         if (o.row_block == 0) o.row_block = 16;
         if (o.ndev == 0) o.ndev = 1;
+        if (opts->struct_size < offsetof(rt_opts, spp) + sizeof(o.spp) || o.spp == 0) o.spp = 1; // ABI 1 callers
     }
     int rc = check_scene(scene, n);
     if (rc != RT_OK) return rc;
@@ -1419,7 +1454,8 @@ int rt_render(const rt_elem *scene, uint32_t n, uint32_t width, uint32_t height,
             break;
         }
         (void)hipEventRecord(dv.e0, dv.st);
-        err = rt_launch(dv.p, width, height, depth, rb, s, ns, o.precision, o.order, dv.d_out, dv.d_lv, dv.st);
+        err = rt_launch_spp(dv.p, width, height, depth, rb, s, ns, o.precision, o.order, o.spp, o.seed, dv.d_out,
+                            dv.d_lv, dv.st);
         if (err != RT_OK) break;
         (void)hipEventRecord(dv.e1, dv.st);
         err = scatter_slab(static_cast<const char *>(dv.d_out), rowbytes, height, rb, s, ns,

@@ -74,12 +74,13 @@ class FrameRenderer:
 
     def __init__(self, scene, width: int, height: int, depth: int, *, rank: int = 0, world: int = 1,
                  device: int = 0, row_block: int = 16, precision: str = "f32", order: str = "exact", group=None,
-                 levels: bool = False):
+                 levels: bool = False, spp: int = 1, seed: int = 0):
         import torch
         self.torch = torch
         self.L = N.lib()
         self.w, self.h, self.depth = width, height, depth
         self.rank, self.world, self.rb, self.group = rank, world, row_block, group
+        self.spp, self.seed = spp, seed
         self.prec, self.order = PRECISIONS[precision], ORDERS[order]
         self.dtype = torch.float64 if precision == "f64" else torch.float32
         self.device = torch.device("cuda", device)
@@ -98,8 +99,8 @@ class FrameRenderer:
     def launch(self):
         st = self.torch.cuda.current_stream(self.device).cuda_stream
         lv = self.levels.data_ptr() if self.levels is not None else None
-        N.check(self.L.rt_launch(self._p, self.w, self.h, self.depth, self.rb, self.rank, self.world, self.prec,
-                                 self.order, self.slab.data_ptr(), lv, st), "rt_launch")
+        N.check(self.L.rt_launch_spp(self._p, self.w, self.h, self.depth, self.rb, self.rank, self.world, self.prec,
+                                     self.order, self.spp, self.seed, self.slab.data_ptr(), lv, st), "rt_launch")
 
     def gather(self):
         if self.world == 1:

@@ -54,9 +54,11 @@ def _depth_ok(depth):
 
 def render(width: int, height: int, scene=None, depth: int = 5, *, precision: str = "f64",
            order: str = "exact", ndev: int = 1, first_dev: int = 0, row_block: int = 16,
-           levels: bool = False, stats: dict | None = None):
+           levels: bool = False, stats: dict | None = None, spp: int = 1, seed: int = 0):
     """Render through ``rt_render`` and return a ``(height, width, 3)`` array (float64 or
-    float32), plus the per-pixel levels array if ``levels``.  ``'done'`` for 0x0."""
+    float32), plus the per-pixel levels array if ``levels``.  ``'done'`` for 0x0.
+    ``spp`` > 1: stochastic supersampling as defined at RT_SUPERSAMPLING in
+    include/rt_mi355x.h (not in the reference; levels then report sample 0)."""
     if not _sizes_ok(width, height):
         return DONE
     _depth_ok(depth)
@@ -70,7 +72,7 @@ def render(width: int, height: int, scene=None, depth: int = 5, *, precision: st
     lv = np.empty((height, width), dtype=np.uint8) if levels else None
     opts = N.RtOpts(ctypes.sizeof(N.RtOpts), first_dev, ndev, prec,
                     {"exact": N.RT_ORDER_EXACT, "fast": N.RT_ORDER_FAST}[order], row_block,
-                    lv.ctypes.data if levels else None)
+                    lv.ctypes.data if levels else None, spp, 0, seed)
     st = N.RtStats()
     rc = L.rt_render(elems, len(elems), width, height, depth, ctypes.byref(opts), out.ctypes.data, ctypes.byref(st))
     if rc == N.RT_DONE:

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* ---- return codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -107,7 +107,24 @@ typedef struct rt_opts {
     int32_t order;        /* RT_ORDER_EXACT (default) or RT_ORDER_FAST */
     uint32_t row_block;   /* multi-device interleave granularity in rows (default 16) */
     uint8_t *out_levels;  /* optional host W*H bytes: reflection-chain levels that hit, per pixel */
+    /* appended in ABI 2 (older callers' smaller struct_size leaves the defaults) */
+    uint32_t spp;         /* samples per pixel (default 1 = the reference; see RT_SUPERSAMPLING) */
+    uint32_t reserved0;
+    uint64_t seed;        /* jitter seed for spp > 1 */
 } rt_opts;
+
+/* RT_SUPERSAMPLING — stochastic supersampling (BASELINE.json config 5; the reference has
+ * none, so this definition is the contract and the oracle restates it).  With spp > 1,
+ * sample s (0 <= s < spp) of pixel (x, y), pixel = y*W + x in the whole image:
+ *     r = splitmix64(seed ^ (pixel*spp + s)),
+ *         splitmix64(z): z += 0x9E3779B97F4A7C15; z = (z ^ z>>30) * 0xBF58476D1CE4E5B9;
+ *                        z = (z ^ z>>27) * 0x94D049BB133111EB; return z ^ z>>31;
+ *     u = (r >> 40) * 2^-24,  v = ((r >> 16) & 0xFFFFFF) * 2^-24      (24-bit fractions)
+ *     X = (x + u) / W,  Y = (y + v) / H                                 (binary64)
+ * and the pixel is (c_0 + c_1 + ... + c_{spp-1}) / spp, summed left to right in binary64.
+ * spp = 1 is the reference's X = x/W, Y = y/H exactly.  out_levels / d_levels report
+ * sample 0. */
+#define RT_MAX_SPP 4096
 
 typedef struct rt_stats {
     double kernel_ms;   /* device time of the render kernels (max over devices) */
@@ -152,6 +169,10 @@ uint32_t rt_shard_rows(uint32_t height, uint32_t row_block, uint32_t nshards);
 int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth,
               uint32_t row_block, uint32_t shard, uint32_t nshards, int precision, int order,
               void *d_out, uint8_t *d_levels, void *stream);
+/* rt_launch with spp samples per pixel (RT_SUPERSAMPLING); spp = 1 is rt_launch. */
+int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth,
+                  uint32_t row_block, uint32_t shard, uint32_t nshards, int precision, int order,
+                  uint32_t spp, uint64_t seed, void *d_out, uint8_t *d_levels, void *stream);
 /* Reassemble nshards gathered slabs (d_slabs = [nshards][shard_rows][W*3]) into the
  * row-major image d_image ([H][W*3]), on `stream`. */
 int rt_unshard(const void *d_slabs, uint32_t width, uint32_t height, uint32_t row_block,

@@ -39,6 +39,9 @@ def lib():
         L.orc_render.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                  ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                  ctypes.c_void_p]
+        L.orc_render_spp.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_focal_length.restype = ctypes.c_double
         L.orc_focal_length.argtypes = [ctypes.c_double, ctypes.c_double]
         L.orc_vec_op.argtypes = [ctypes.c_int, dp, dp, ctypes.c_double, dp]
@@ -56,17 +59,18 @@ def _d3(v):
     return (ctypes.c_double * 3)(*[float(x) for x in v])
 
 
-def render(elems, width, height, depth, mode=MEMO, threads=None, row0=0, nrows=None, levels=False):
+def render(elems, width, height, depth, mode=MEMO, threads=None, row0=0, nrows=None, levels=False, spp=1, seed=0):
     """Render rows [row0, row0+nrows) of a width x height image of the marshalled scene
-    `elems`; returns a (nrows, width, 3) float64 array (and the levels array)."""
+    `elems`; returns a (nrows, width, 3) float64 array (and the levels array).  spp > 1:
+    stochastic supersampling as defined at RT_SUPERSAMPLING in include/rt_mi355x.h."""
     if nrows is None:
         nrows = height - row0
     if threads is None:
         threads = os.cpu_count() or 1
     out = np.zeros((nrows, width, 3), dtype=np.float64)
     lv = np.zeros((nrows, width), dtype=np.uint8) if levels else None
-    rc = lib().orc_render(ctypes.cast(elems, ctypes.c_void_p), len(elems), width, height, row0, nrows, depth, mode,
-                          threads, out.ctypes.data, lv.ctypes.data if levels else None)
+    rc = lib().orc_render_spp(ctypes.cast(elems, ctypes.c_void_p), len(elems), width, height, row0, nrows, depth,
+                              mode, threads, spp, seed, out.ctypes.data, lv.ctypes.data if levels else None)
     if rc != 0:
         raise ValueError(f"oracle render failed: {rc}")
     return (out, lv) if levels else out

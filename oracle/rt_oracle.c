@@ -360,7 +360,17 @@ typedef struct {
     double *out;
     uint8_t *levels;
     volatile uint32_t *next;
+    uint32_t spp;
+    uint64_t seed;
 } Job;
+
+/* RT_SUPERSAMPLING (include/rt_mi355x.h; not part of the reference): the jitter hash. */
+static uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
 
 static void *worker(void *arg) {
     Job *j = (Job *)arg;
@@ -370,9 +380,29 @@ static void *worker(void *arg) {
         uint32_t y = j->row0 + r;
         for (uint32_t x = 0; x < j->W; x++) {
             int lv = 0;
-            /* {X/Width, Y/Height}: float division of the integer pixel indices */
-            V c = trace_ray_through_pixel((double)x / (double)j->W, (double)y / (double)j->H, j->sc, j->depth,
-                                          j->mode, &lv);
+            V c;
+            if (j->spp <= 1) {
+                /* {X/Width, Y/Height}: float division of the integer pixel indices */
+                c = trace_ray_through_pixel((double)x / (double)j->W, (double)y / (double)j->H, j->sc, j->depth,
+                                            j->mode, &lv);
+            } else {
+                /* sample s at ((x+u)/W, (y+v)/H); the samples summed left to right, then / spp */
+                const uint64_t pixel = (uint64_t)y * j->W + x;
+                for (uint32_t s = 0; s < j->spp; s++) {
+                    const uint64_t h = splitmix64(j->seed ^ (pixel * j->spp + s));
+                    const double u = (double)(h >> 40) * 0x1p-24, v = (double)((h >> 16) & 0xFFFFFFull) * 0x1p-24;
+                    int ls = 0;
+                    const V cs = trace_ray_through_pixel(((double)x + u) / (double)j->W, ((double)y + v) / (double)j->H,
+                                                         j->sc, j->depth, j->mode, &ls);
+                    if (s == 0) {
+                        c = cs;
+                        lv = ls;
+                    } else {
+                        c.x = c.x + cs.x; c.y = c.y + cs.y; c.z = c.z + cs.z;
+                    }
+                }
+                c.x = c.x / (double)j->spp; c.y = c.y / (double)j->spp; c.z = c.z / (double)j->spp;
+            }
             size_t o = ((size_t)r * j->W + x);
             j->out[o * 3 + 0] = c.x; j->out[o * 3 + 1] = c.y; j->out[o * 3 + 2] = c.z;
             if (j->levels) j->levels[o] = (uint8_t)lv;
@@ -381,15 +411,16 @@ static void *worker(void *arg) {
     return NULL;
 }
 
-/* Render rows [row0, row0+nrows) of a W x H image into out (nrows*W*3 doubles). */
-int orc_render(const rt_elem *scene, uint32_t n, uint32_t W, uint32_t H, uint32_t row0, uint32_t nrows,
-               int depth, int mode, int threads, double *out, uint8_t *levels) {
+/* Render rows [row0, row0+nrows) of a W x H image into out (nrows*W*3 doubles), spp
+ * samples per pixel (RT_SUPERSAMPLING; spp = 1 is the reference's pixel loop). */
+int orc_render_spp(const rt_elem *scene, uint32_t n, uint32_t W, uint32_t H, uint32_t row0, uint32_t nrows,
+                   int depth, int mode, int threads, uint32_t spp, uint64_t seed, double *out, uint8_t *levels) {
     if (n < 1 || scene[0].kind != RT_CAMERA) return RT_EBADARG;
     if (W == 0 || H == 0) return (W == 0 && H == 0) ? RT_DONE : RT_EBADARG;
     if (row0 + nrows > H) return RT_EBADARG;
     Scene sc = {scene, n};
     volatile uint32_t next = 0;
-    Job job = {&sc, W, H, row0, nrows, depth, mode, out, levels, &next};
+    Job job = {&sc, W, H, row0, nrows, depth, mode, out, levels, &next, spp ? spp : 1, seed};
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
     pthread_t tid[256];
@@ -397,4 +428,9 @@ int orc_render(const rt_elem *scene, uint32_t n, uint32_t W, uint32_t H, uint32_
     worker(&job);
     for (int t = 1; t < threads; t++) pthread_join(tid[t], NULL);
     return RT_OK;
+}
+
+int orc_render(const rt_elem *scene, uint32_t n, uint32_t W, uint32_t H, uint32_t row0, uint32_t nrows,
+               int depth, int mode, int threads, double *out, uint8_t *levels) {
+    return orc_render_spp(scene, n, W, H, row0, nrows, depth, mode, threads, 1, 0, out, levels);
 }

@@ -41,7 +41,7 @@ def test_library_targets_gfx950():
 
 def test_abi_version_and_errors(native):
     L = native.lib()
-    assert L.rt_abi_version() == 1
+    assert L.rt_abi_version() == 2
     for code in (N.RT_OK, N.RT_DONE, N.RT_EBADARG, N.RT_ENODEV, N.RT_EHIP, N.RT_ENOMEM, N.RT_ETOOBIG):
         assert N.strerror(code) and N.strerror(code) != "unknown error"
     assert N.strerror(-99) == "unknown error"
@@ -53,8 +53,8 @@ def test_struct_layout_matches_header():
 #include <stdio.h>
 #include <stddef.h>
 #include "rt_mi355x.h"
-int main(void){printf("%zu %zu %zu %zu %zu\n", sizeof(rt_elem), sizeof(rt_opts), sizeof(rt_stats),
- offsetof(rt_elem, u), offsetof(rt_opts, out_levels)); return 0;}
+int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(rt_elem), sizeof(rt_opts), sizeof(rt_stats),
+ offsetof(rt_elem, u), offsetof(rt_opts, out_levels), offsetof(rt_opts, spp), offsetof(rt_opts, seed)); return 0;}
 '''
     import tempfile
     with tempfile.TemporaryDirectory() as d:
@@ -64,7 +64,7 @@ int main(void){printf("%zu %zu %zu %zu %zu\n", sizeof(rt_elem), sizeof(rt_opts),
         subprocess.run(["gcc", "-I", os.path.dirname(HEADER), c, "-o", exe], check=True)
         got = list(map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()))
     assert got == [ctypes.sizeof(N.RtElem), ctypes.sizeof(N.RtOpts), ctypes.sizeof(N.RtStats),
-                   N.RtElem.u.offset, N.RtOpts.out_levels.offset]
+                   N.RtElem.u.offset, N.RtOpts.out_levels.offset, N.RtOpts.spp.offset, N.RtOpts.seed.offset]
 
 
 def test_scene_check(native):

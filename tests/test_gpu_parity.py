@@ -190,3 +190,46 @@ def test_repeated_launch_graph_replay(oracle):
         _check(big.cpu().numpy(), refb)
     finally:
         L.rt_release(p)
+
+
+@pytest.mark.parametrize("name,w,h,d,spp", [("s64", 48, 40, 5, 4), ("default", 40, 32, 5, 3), ("s256", 32, 24, 8, 16)])
+def test_supersampling_matches_oracle(oracle, name, w, h, d, spp):
+    """BASELINE config 5's stochastic supersampling (RT_SUPERSAMPLING) against the oracle's
+    restatement of the same definition; levels are sample 0's."""
+    scene = scenes.named(name)
+    seed = 0x5EED0005
+    img, lv = render(w, h, scene, d, levels=True, spp=spp, seed=seed)
+    ref, rlv = oracle.render(N.marshal(scene), w, h, d, mode=oracle.MEMO, levels=True, spp=spp, seed=seed)
+    np.testing.assert_array_equal(lv, rlv)
+    _check(img, ref)
+    f32 = render(w, h, scene, d, precision="f32", spp=spp, seed=seed)
+    _check(f32, ref)
+
+
+def test_supersampling_shards():
+    """rt_launch_spp per shard + rt_unshard equals the single-shard supersampled frame."""
+    import torch
+    L = N.lib()
+    el = N.marshal(scenes.s64())
+    w, h, d, rb, spp, seed = 64, 50, 5, 16, 4, 77
+    p = ctypes.c_void_p()
+    N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(p)), "rt_prepare")
+    try:
+        st = torch.cuda.current_stream().cuda_stream
+        full = torch.empty((h, w, 3), dtype=torch.float64, device="cuda")
+        N.check(L.rt_launch_spp(p, w, h, d, rb, 0, 1, N.RT_OUT_F64, N.RT_ORDER_EXACT, spp, seed, full.data_ptr(),
+                                None, st))
+        ns = 3
+        rows = L.rt_shard_rows(h, rb, ns)
+        slabs = torch.zeros((ns, rows, w, 3), dtype=torch.float64, device="cuda")
+        for s in range(ns):
+            N.check(L.rt_launch_spp(p, w, h, d, rb, s, ns, N.RT_OUT_F64, N.RT_ORDER_EXACT, spp, seed,
+                                    slabs[s].data_ptr(), None, st))
+        img = torch.empty_like(full)
+        N.check(L.rt_unshard(slabs.data_ptr(), w, h, rb, ns, N.RT_OUT_F64, img.data_ptr(), st))
+        torch.cuda.synchronize()
+        assert torch.equal(img, full)
+        assert L.rt_launch_spp(p, w, h, d, rb, 0, 1, N.RT_OUT_F64, N.RT_ORDER_EXACT, 0, seed, full.data_ptr(), None,
+                               st) == N.RT_EBADARG
+    finally:
+        L.rt_release(p)

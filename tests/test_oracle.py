@@ -198,3 +198,37 @@ def test_golden_scene_files():
     for name in ("default", "s64", "s256"):
         t = terms.consult(os.path.join(GOLDEN, f"scene_{name}.eterm"))[0]
         assert terms.exact_eq(t, scenes.named(name)), name
+
+
+def test_supersampling_definition(oracle):
+    """RT_SUPERSAMPLING (include/rt_mi355x.h; not in the reference, so parity is against this
+    definition): the oracle's supersampled pixels equal an independent Python evaluation of
+    the jittered sample positions, traced one by one and summed in sample order."""
+    import numpy as np
+    from eraytracer_amd import _native as N
+    from eraytracer_amd import scenes
+    M = (1 << 64) - 1
+
+    def splitmix64(z):
+        z = (z + 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    el = N.marshal(scenes.s64())
+    W, H, D, spp, seed = 9, 7, 5, 3, 0xC0FFEE
+    img, lv = oracle.render(el, W, H, D, spp=spp, seed=seed, levels=True)
+    assert np.array_equal(oracle.render(el, W, H, D, spp=1, seed=seed), oracle.render(el, W, H, D))
+    for y in range(H):
+        for x in range(W):
+            acc = None
+            for s in range(spp):
+                r = splitmix64(seed ^ ((y * W + x) * spp + s))
+                u, v = (r >> 40) * 2.0 ** -24, ((r >> 16) & 0xFFFFFF) * 2.0 ** -24
+                c, lev = oracle.trace_pixel(el, (x + u) / W, (y + v) / H, D)
+                if s == 0:
+                    acc, lev0 = list(c), lev
+                else:
+                    acc = [acc[i] + c[i] for i in range(3)]
+            assert [a / spp for a in acc] == list(img[y, x])
+            assert lev0 == lv[y, x]
