@@ -143,7 +143,7 @@ static ERL_NIF_TERM rt_error(ErlNifEnv *env, int rc) {
 
 /* shared front half: parse args, render into a double buffer */
 static ERL_NIF_TERM render_common(ErlNifEnv *env, const ERL_NIF_TERM argv[], unsigned *W, unsigned *H,
-                                  double **buf, int *done, int all_devices) {
+                                  double **buf, int *done, int all_devices, unsigned spp, ErlNifUInt64 seed) {
     unsigned D, n = 0;
     rt_elem *elems = NULL;
     ERL_NIF_TERM *terms = NULL, err = 0;
@@ -173,6 +173,8 @@ static ERL_NIF_TERM render_common(ErlNifEnv *env, const ERL_NIF_TERM argv[], uns
     o.precision = RT_OUT_F64;
     o.order = RT_ORDER_EXACT;
     o.row_block = 16;
+    o.spp = spp;   /* RT_SUPERSAMPLING (include/rt_mi355x.h); 1 = the reference's pixel */
+    o.seed = seed;
     rc = rt_render(elems, n, *W, *H, D, &o, *buf, NULL);
     if (rc < 0) {
         enif_free(*buf);
@@ -195,7 +197,7 @@ static ERL_NIF_TERM render_nif(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
     else if (enif_is_identical(argv[4], atom_indexed)) keyed = 1;
     else if (enif_is_identical(argv[4], atom_distributed)) keyed = all = 1;
     else return enif_make_badarg(env);
-    ERL_NIF_TERM r = render_common(env, argv, &W, &H, &buf, &done, all);
+    ERL_NIF_TERM r = render_common(env, argv, &W, &H, &buf, &done, all, 1, 0);
     if (done || !buf) return r;
     ERL_NIF_TERM list = enif_make_list(env, 0), one = enif_make_int(env, 1);
     for (size_t i = (size_t)W * H; i-- > 0;) {
@@ -209,14 +211,24 @@ static ERL_NIF_TERM render_nif(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
     return list;
 }
 
-/* render_binary(W, H, Scene, Depth) -> <<R:64/float-native, G, B, ...>> row-major */
+/* render_binary(W, H, Scene, Depth) -> <<R:64/float-native, G, B, ...>> row-major
+ * render_binary(W, H, Scene, Depth, #{spp => N, seed => S}) -> the same, supersampled */
 static ERL_NIF_TERM render_binary_nif(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
-    unsigned W, H;
+    unsigned W, H, spp = 1;
+    ErlNifUInt64 seed = 0;
     double *buf;
     int done;
     ErlNifBinary bin;
-    (void)argc;
-    ERL_NIF_TERM r = render_common(env, argv, &W, &H, &buf, &done, 0);
+    if (argc == 5) {
+        ERL_NIF_TERM v;
+        if (!enif_is_map(env, argv[4])) return enif_make_badarg(env);
+        if (enif_get_map_value(env, argv[4], enif_make_atom(env, "spp"), &v) && !enif_get_uint(env, v, &spp))
+            return enif_make_badarg(env);
+        if (enif_get_map_value(env, argv[4], enif_make_atom(env, "seed"), &v) && !enif_get_uint64(env, v, &seed))
+            return enif_make_badarg(env);
+        if (spp == 0) return enif_make_badarg(env);
+    }
+    ERL_NIF_TERM r = render_common(env, argv, &W, &H, &buf, &done, 0, spp, seed);
     if (done || !buf) return r;
     size_t nb = (size_t)W * H * 3 * sizeof(double);
     if (!enif_alloc_binary(nb, &bin)) {
@@ -231,6 +243,7 @@ static ERL_NIF_TERM render_binary_nif(ErlNifEnv *env, int argc, const ERL_NIF_TE
 static ErlNifFunc funcs[] = {
     {"render", 5, render_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"render_binary", 4, render_binary_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"render_binary", 5, render_binary_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
 };
 
 ERL_NIF_INIT(rt_nif, funcs, load, NULL, NULL, NULL)

@@ -1,6 +1,6 @@
 %% rt_nif.erl — Erlang side of the NIF in erlang/c_src/rt_nif.c.
 -module(rt_nif).
--export([render/5, render_binary/4]).
+-export([render/5, render_binary/4, render_binary/5]).
 -on_load(init/0).
 
 init() ->
@@ -16,4 +16,9 @@ render(_Width, _Height, _Scene, _Depth, _KeyMode) ->
 
 %% render_binary(Width, Height, Scene, Depth) -> done | binary()
 render_binary(_Width, _Height, _Scene, _Depth) ->
+    erlang:nif_error(nif_not_loaded).
+
+%% render_binary(Width, Height, Scene, Depth, #{spp => N, seed => S}) -> done | binary()
+%% Stochastic supersampling as defined at RT_SUPERSAMPLING in include/rt_mi355x.h.
+render_binary(_Width, _Height, _Scene, _Depth, _Opts) ->
     erlang:nif_error(nif_not_loaded).
