@@ -611,6 +611,9 @@ __device__ __forceinline__ Target make_target(const Scene &S, int obj, bool acti
     return T;
 }
 
+// SPH: the scene holds only spheres and culling is on (host-checked), so every target is a
+// sphere with occluder masks: the cone and triangle/plane paths are compiled out (registers).
+template <bool SPH = false>
 __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &T, const D3 &sd, bool active,
                                        const HitBall &hb, const D3 &Lp) {
     const SceneHdr &h = S.h;
@@ -621,7 +624,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
     double ts = 0;
     bool valid = false;
     if (active) {
-        if (kind == K_SPHERE) {
+        if (SPH || kind == K_SPHERE) {
             const double *q = S.tab + h.o_sph_org + (org * h.n_sph + loc) * SPH_ORG_W;
             double B = 2 * (sd.x * q[0] + sd.y * q[1] + sd.z * q[2]);
             valid = sph_t(B, q[3], A4, ts);
@@ -640,11 +643,11 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
     // Candidate occluders.  Sphere targets: the union of the host-precomputed occluder masks of
     // the wave's distinct targets (no reductions).  Otherwise the cone from the light to the
     // hit ball of the wave, culled lane-parallel.
-    const bool sph_targets = h.cull_ok && __ballot(!blocked && kind != K_SPHERE) == 0;
+    const bool sph_targets = SPH || (h.cull_ok && __ballot(!blocked && kind != K_SPHERE) == 0);
     double tmax = __builtin_inf();
     Beam b;
     b.on = false;
-    if (!sph_targets) b = shadow_cone(hb, Lp, tmax); // shadow rays all start at the light
+    if (!SPH && !sph_targets) b = shadow_cone(hb, Lp, tmax); // shadow rays all start at the light
     RT_STAT(ST_SHADOW, 1);
     RT_STAT(ST_SHADOW_CONE_ON, (sph_targets || b.on) ? 1 : 0);
     for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
@@ -672,12 +675,12 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
             }
             if (__all(blocked)) return false;
             continue;
-        } else {
+        } else if (!SPH) {
             m = b.on ? cull_chunk(S, b, chunk, org, tmax) : chunk_all(h.n_sph, chunk);
             if (skip >= chunk && skip < chunk + 64) m &= ~(1ull << (skip - chunk));
         }
         RT_STAT(ST_SHADOW_CAND, __popcll(m));
-        while (m) {
+        while (!SPH && m) {
             const int k = chunk + __builtin_ctzll(m);
             m &= m - 1;
             RT_STAT(ST_SHADOW_ITER, 1);
@@ -690,6 +693,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
             if (__all(blocked)) return false;
         }
     }
+    if (SPH) return !blocked;
     for (int k = 0; k < h.n_tri; ++k) {
         if (!blocked) {
             const double *g = S.tab + h.o_tri + k * TRI_W;
@@ -723,7 +727,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
 // re-read per light for the same reason.
 // bits (optional): bit i set where light i's shadow test passed (lights 0..31; only lanes whose
 // light term is not exactly zero are tested, the others' bits are 0 and never matter).
-template <bool GENPOW>
+template <bool GENPOW, bool SPH = false>
 __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D3 &hit, const D3 &N, const D3 &col,
                                     double refl, bool active, unsigned *bits = nullptr) {
     const SceneHdr &h = S.h;
@@ -734,7 +738,7 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
     HitBall hb;
     hb.on = false;
     hb.cx = hb.cy = hb.cz = hb.r = 0.0;
-    if (__ballot(active && T.kind != K_SPHERE) != 0) hb = make_hitball(h, active, hit);
+    if (!SPH && __ballot(active && T.kind != K_SPHERE) != 0) hb = make_hitball(h, active, hit);
     RT_STAT(ST_SHADE, 1);
     D3 F = {0.0, 0.0, 0.0};
     for (int i = 0; i < h.n_light; ++i) {
@@ -757,7 +761,7 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
         const D3 lc = {Lc.x * con.x, Lc.y * con.y, Lc.z * con.z};
         const bool need = active && !(lc.x == 0.0 && lc.y == 0.0 && lc.z == 0.0);
         // shadow ray direction normalize(Hit - Light) == -normalize(Light - Hit), bit for bit
-        const bool lb = lit_by(S, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp);
+        const bool lb = lit_by<SPH>(S, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp);
         if (bits && lb && i < 32) *bits |= 1u << i;
         const double lit = lb ? 1.0 : 0.0;
         F.x = F.x + (col.x * refl + lc.x * lit);
@@ -1146,6 +1150,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     HitRec *q = static_cast<HitRec *>(p->d_queue);
     const int nrefl = (p->hdr.n_light > 0 && D > 1) ? D - 1 : 0;
     const int nshade = D > 0 ? 1 + nrefl : 0;
+    // spheres only, culling on: every shadow target has occluder masks (lit_by<true>)
+    const bool sph_only = p->hdr.n_tri == 0 && p->hdr.n_pl == 0 && p->hdr.cull_ok;
     for (int row0 = 0; row0 < slab_rows; row0 += pass_rows) {
         const int rows = std::min(pass_rows, slab_rows - row0);
         const int ntiles = tiles_x * ((rows + TILE - 1) / TILE);
@@ -1179,8 +1185,12 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                 HIPCHK(hipEventRecord(p->ev_level[k], st));
                 HIPCHK(hipStreamWaitEvent(ls(k), p->ev_level[k], 0));
             }
-            hipLaunchKernelGGL((k_light<PREC, GENPOW>), dim3(sblocks), dim3(BLOCK), 0, ls(k), p->hdr, p->d_tab,
-                               p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k));
+            if (sph_only)
+                hipLaunchKernelGGL((k_light<PREC, GENPOW, true>), dim3(sblocks), dim3(BLOCK), 0, ls(k), p->hdr,
+                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k));
+            else
+                hipLaunchKernelGGL((k_light<PREC, GENPOW, false>), dim3(sblocks), dim3(BLOCK), 0, ls(k), p->hdr,
+                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k));
             HIPCHK(hipGetLastError());
             if (overlap) HIPCHK(hipEventRecord(p->ev_lit[k], ls(k)));
             return RT_OK;
