@@ -342,39 +342,69 @@ __device__ __forceinline__ unsigned long long chunk_all(int n_sph, int chunk) {
 }
 
 // The sphere candidates in mask m of chunk `chunk`, folded into the running nearest (bt, bid).
+// Two candidates per step: the (t, list position) minimum does not depend on the order the
+// candidates are visited, and the two tests are independent, which gives the wave
+// instruction-level parallelism across the scalar loads and the root computations.
 template <bool PRE>
+__device__ __forceinline__ void sphere_BC(const Scene &S, int org, const D3 &o, const D3 &d, int k, double &B,
+                                          double &C) {
+    const SceneHdr &h = S.h;
+    if (PRE) {
+        const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
+        B = 2 * (d.x * q[0] + d.y * q[1] + d.z * q[2]);
+        C = q[3];
+    } else {
+        const double *s = S.tab + h.o_sph + k * SPH_W;
+        D3 oc = {o.x - s[0], o.y - s[1], o.z - s[2]};
+        B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
+        C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - s[3];
+    }
+}
+// ILP = false: one candidate per step (the least work: dense, throughput-bound waves).
+template <bool PRE, bool ILP = false>
 __device__ __forceinline__ void scan_spheres(const Scene &S, int org, const D3 &o, const D3 &d, double A4, int chunk,
                                              unsigned long long m, double &bt, int &bid) {
     const SceneHdr &h = S.h;
     RT_STAT(PRE ? ST_NEAR_PRE_CAND : ST_NEAR_GEN_CAND, __popcll(m));
-    while (m) {
+    while (!ILP && m) {
         const int k = chunk + __builtin_ctzll(m);
         m &= m - 1;
         double B, C;
-        if (PRE) {
-            const double *q = S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W;
-            B = 2 * (d.x * q[0] + d.y * q[1] + d.z * q[2]);
-            C = q[3];
-        } else {
-            const double *s = S.tab + h.o_sph + k * SPH_W;
-            D3 oc = {o.x - s[0], o.y - s[1], o.z - s[2]};
-            B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
-            C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - s[3];
-        }
+        sphere_BC<PRE>(S, org, o, d, k, B, C);
         const int id = S.itab[h.i_sph_id + k];
         double t;
         const bool upd = (int)sph_t_wave(B, C, A4, t) & (int)nearer(t, id, bt, bid);
         bt = upd ? t : bt;
         bid = upd ? id : bid;
     }
+    while (ILP && m) {
+        const int k0 = chunk + __builtin_ctzll(m);
+        m &= m - 1;
+        const bool two = m != 0;
+        const int k1 = two ? chunk + __builtin_ctzll(m) : k0;
+        if (two) m &= m - 1;
+        double B0, C0, B1, C1;
+        sphere_BC<PRE>(S, org, o, d, k0, B0, C0);
+        sphere_BC<PRE>(S, org, o, d, k1, B1, C1);
+        const int id0 = S.itab[h.i_sph_id + k0], id1 = S.itab[h.i_sph_id + k1];
+        // sph_t for both, without divergent branches; the roots only if some lane can hit
+        const double disc0 = B0 * B0 - A4 * C0, disc1 = B1 * B1 - A4 * C1;
+        const bool ok0 = disc0 >= 0.001, ok1 = disc1 >= 0.001;
+        if (__ballot(ok0 | ok1) == 0) continue;
+        const double sq0 = sqrt(ok0 ? disc0 : 1.0), sq1 = sqrt(ok1 ? disc1 : 1.0);
+        const double a0 = (-B0 + sq0) / 2, b0 = (-B0 - sq0) / 2;
+        const double a1 = (-B1 + sq1) / 2, b1 = (-B1 - sq1) / 2;
+        const double t0 = (b0 < a0) ? b0 : a0, t1 = (b1 < a1) ? b1 : a1;
+        const bool h0 = ok0 & (a0 >= 0) & (b0 >= 0), h1 = two & ok1 & (a1 >= 0) & (b1 >= 0);
+        const bool u0 = h0 & nearer(t0, id0, bt, bid);
+        bt = u0 ? t0 : bt;
+        bid = u0 ? id0 : bid;
+        const bool u1 = h1 & nearer(t1, id1, bt, bid);
+        bt = u1 ? t1 : bt;
+        bid = u1 ? id1 : bid;
+    }
 }
 
-// nearest_object_intersecting_ray/6 (:303-346).  PRE: the ray starts at origin slot `org`
-// (tabled); otherwise at o, on object `grp` (the previous hit, or -1).  Returns the compact
-// object id (-1 = none) and its t.  Called by the whole wave; `act` marks the traced lanes.
-// Reflection rays are culled per group of lanes leaving the same object (at most
-// MAX_GROUPS beams, the last one covering every remaining lane): lanes on different objects
-// would otherwise share one wide beam.  Testing a sphere twice cannot change the nearest.
 // The triangles and planes of the scene, folded into the running nearest (bt, bid).
 template <bool PRE>
 __device__ __forceinline__ void scan_tri_pl(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, int &bid) {
@@ -410,7 +440,7 @@ __device__ __forceinline__ void scan_tri_pl(const Scene &S, int org, const D3 &o
 }
 
 constexpr int MAX_GROUPS = 3;
-template <bool PRE>
+template <bool PRE, bool ILP = false>
 __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, bool act,
                                        int grp = -1) {
     const SceneHdr &h = S.h;
@@ -421,6 +451,27 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
     RT_STAT(PRE ? ST_NEAR_PRE : ST_NEAR_GEN, 1);
     RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
     unsigned long long rem = __ballot(act);
+    if (!PRE && h.n_sph <= 64) {
+        // One chunk: the union of the groups' candidate masks, walked once by the whole wave
+        // (a sphere outside a lane's cone cannot be hit by that lane, so testing it is harmless).
+        unsigned long long m = 0;
+        bool all = false;
+        for (int g = 0; g < MAX_GROUPS && rem; ++g) {
+            const int gv = __builtin_amdgcn_readlane(grp, __builtin_ctzll(rem));
+            const bool sel = (g == MAX_GROUPS - 1) ? ((rem >> (threadIdx.x & 63)) & 1) != 0 : (act && grp == gv);
+            rem &= ~__ballot(sel);
+            const Beam b = make_beam(h, sel, o, d, false);
+            RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
+            if (!b.on) {
+                all = true;
+                break;
+            }
+            m |= cull_chunk(S, b, 0, -1);
+        }
+        if (all) m = chunk_all(h.n_sph, 0);
+        scan_spheres<false, ILP>(S, org, o, d, A4, 0, m, bt, bid);
+        rem = 0;
+    }
     for (int g = 0; g < MAX_GROUPS && rem; ++g) {
         bool sel = act;
         if (!PRE) {
@@ -433,7 +484,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
         for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
             const unsigned long long m =
                 b.on ? cull_chunk(S, b, chunk, PRE ? org : -1) : chunk_all(h.n_sph, chunk);
-            scan_spheres<PRE>(S, org, o, d, A4, chunk, m, bt, bid);
+            scan_spheres<PRE, ILP>(S, org, o, d, A4, chunk, m, bt, bid);
         }
         if (!b.on) break; // everything was scanned
     }
@@ -1197,12 +1248,20 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         };
         if (nshade > 0 && (rc = level_lists(0)) != RT_OK) return rc;
         for (int k = 1; k <= nrefl; ++k) {
-            if (lv)
-                hipLaunchKernelGGL((k_reflect<true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
-                                   k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+            // level 1 (from the primary hits) is dense and throughput-bound; deeper levels are a few
+            // waves each, bound by one wave's dependent chain: they walk two candidates per step
+            if (lv && k == 1)
+                hipLaunchKernelGGL((k_reflect<true, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+            else if (lv)
+                hipLaunchKernelGGL((k_reflect<true, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+            else if (k == 1)
+                hipLaunchKernelGGL((k_reflect<false, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
             else
-                hipLaunchKernelGGL((k_reflect<false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
-                                   k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+                hipLaunchKernelGGL((k_reflect<false, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
             HIPCHK(hipGetLastError());
             if ((rc = level_lists(k)) != RT_OK) return rc;
         }
