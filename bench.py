@@ -142,8 +142,28 @@ def main():
     ops_rank = workload.ops_from_levels(hist, args.depth, counts) * args.spp
     px_rank = int(hist.sum())
 
+    # With N > 1 ranks a step is render + gather to rank 0 + reorder; frames are pipelined
+    # (frame i+1 renders while frame i's gather is in flight, dist.SlabPipeline) and the
+    # timed region ends only when every frame is gathered and reordered.
+    pipe = fr.pipeline() if world > 1 else None
+
+    def one_step(e0=None, e1=None):
+        if pipe is not None:
+            fr.slab = pipe.slab
+        if e0 is not None:
+            e0.record()
+        fr.launch()
+        if e1 is not None:
+            e1.record()
+        if pipe is not None:
+            pipe.submit()
+        else:
+            fr.gather()
+
     for _ in range(args.warmup):
-        fr.step()
+        one_step()
+    if pipe is not None:
+        pipe.drain()
     torch.cuda.synchronize()
 
     # kernel-only timing of the render launches (events on the launch stream)
@@ -153,10 +173,9 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record()
-        fr.launch()
-        ev[i][1].record()
-        fr.gather()
+        one_step(*ev[i])
+    if pipe is not None:
+        pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

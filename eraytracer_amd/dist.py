@@ -65,6 +65,54 @@ def gather_frame(slab, height: int, row_block: int, world: int, rank: int, group
     return None
 
 
+class SlabPipeline:
+    """Double-buffered gather of per-rank slabs: frame i's gather runs (async, on the
+    collective's own stream) while frame i+1 renders into the other slab; rank 0 reorders a
+    frame when its gather is complete.
+
+    ``slabs`` are this rank's two slab buffers, ``gbufs`` rank 0's two [world, rows, ...]
+    gather buffers (None elsewhere), ``reorder(gbuf)`` rank 0's reassembly into the frame.
+    Stream order keeps it safe: frame i+2 renders into frame i's slab only after frame i's
+    gather has been waited on, and gathers into frame i's buffer only after its reorder."""
+
+    def __init__(self, world, rank, slabs, gbufs=None, reorder=None, group=None):
+        self.world, self.rank, self.group = world, rank, group
+        self.slabs, self.gbufs, self.reorder = slabs, gbufs, reorder
+        self.i = 0            # frames started
+        self.pending = []     # (work, buffer index) in flight
+
+    @property
+    def slab(self):
+        """The slab the next frame renders into."""
+        return self.slabs[self.i % 2]
+
+    def submit(self):
+        """Start gathering the frame just rendered into ``slab``; finish the previous one."""
+        import torch.distributed as dist
+        b = self.i % 2
+        self.i += 1
+        if self.world == 1:
+            return self.slabs[b]
+        gl = list(self.gbufs[b].unbind(0)) if self.rank == 0 else None
+        work = dist.gather(self.slabs[b], gather_list=gl, dst=0, group=self.group, async_op=True)
+        self.pending.append((work, b))
+        return self.complete() if len(self.pending) > 1 else None
+
+    def complete(self):
+        """Wait for the oldest gather in flight and reorder it (rank 0: returns the frame)."""
+        work, b = self.pending.pop(0)
+        work.wait()
+        if self.rank == 0:
+            return self.reorder(self.gbufs[b])
+        return None
+
+    def drain(self):
+        out = None
+        while self.pending:
+            out = self.complete()
+        return out
+
+
 class FrameRenderer:
     """Renders this rank's rows of a W x H frame on its GPU and gathers the frame to rank 0.
 
@@ -95,6 +143,7 @@ class FrameRenderer:
         if world > 1 and rank == 0:
             self.gather_buf = torch.empty((world, self.rows, width, 3), dtype=self.dtype, device=self.device)
             self.frame = torch.empty((height, width, 3), dtype=self.dtype, device=self.device)
+        self._pipe = None
 
     def launch(self):
         st = self.torch.cuda.current_stream(self.device).cuda_stream
@@ -118,6 +167,32 @@ class FrameRenderer:
     def step(self):
         self.launch()
         return self.gather()
+
+    # ---- pipelined frames (world > 1): render frame i+1 while frame i is gathered ----------
+    def pipeline(self):
+        if self._pipe is None:
+            torch = self.torch
+            slabs = [self.slab, torch.empty_like(self.slab)]
+            gbufs = [self.gather_buf, torch.empty_like(self.gather_buf)] if self.gather_buf is not None else None
+            self._pipe = SlabPipeline(self.world, self.rank, slabs, gbufs, self._reorder, self.group)
+        return self._pipe
+
+    def _reorder(self, gbuf):
+        st = self.torch.cuda.current_stream(self.device).cuda_stream
+        N.check(self.L.rt_unshard(gbuf.data_ptr(), self.w, self.h, self.rb, self.world, self.prec,
+                                  self.frame.data_ptr(), st), "rt_unshard")
+        return self.frame
+
+    def step_pipelined(self):
+        """Render the next frame into the free slab and start its gather; returns the previous
+        frame on rank 0 once its gather has completed (None otherwise).  drain() finishes."""
+        pipe = self.pipeline()
+        self.slab = pipe.slab
+        self.launch()
+        return pipe.submit()
+
+    def drain(self):
+        return self._pipe.drain() if self._pipe is not None else None
 
     def close(self):
         if self._p:

@@ -72,3 +72,42 @@ def test_unshard_is_inverse_of_sharding():
                     seen.append(int(row))
         assert sorted(seen) == list(range(h))  # every row owned by exactly one shard
         assert torch.equal(unshard(slabs, h, rb), img)
+
+
+def _pipe_worker(rank, world, port, out_path, nframes):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eraytracer_amd.dist import SlabPipeline
+    rows = shard_rows(H, RB, world)
+    g = torch.from_numpy(shard_global_rows(H, RB, world, rank))
+    slabs = [torch.zeros((rows, W)), torch.zeros((rows, W))]
+    gbufs = [torch.zeros((world, rows, W)), torch.zeros((world, rows, W))] if rank == 0 else None
+    pipe = SlabPipeline(world, rank, slabs, gbufs, lambda gb: unshard(gb, H, RB).clone())
+    frames = []
+    for f in range(nframes):
+        # "render" frame f: every pixel of global row r holds f*1000 + r (padding rows -1)
+        pipe.slab.copy_(torch.where(g[:, None] >= 0, f * 1000.0 + g[:, None].double(), -1.0).float().expand(rows, W))
+        out = pipe.submit()
+        if out is not None:
+            frames.append(out)
+    out = pipe.drain()
+    if out is not None:
+        frames.append(out)
+    if rank == 0:
+        np.save(out_path, torch.stack(frames).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_pipelined_gather_frames_in_order(tmp_path, world):
+    """SlabPipeline (bench.py's multi-GPU step): frame i+1 renders while frame i is gathered;
+    rank 0 must still get every frame, complete, in order and in row order."""
+    out = str(tmp_path / "frames.npy")
+    nframes = 5
+    mp.spawn(_pipe_worker, args=(world, _free_port(), out, nframes), nprocs=world, join=True)
+    frames = np.load(out)
+    assert frames.shape == (nframes, H, W)
+    for f in range(nframes):
+        expect = (f * 1000.0 + np.arange(H, dtype=np.float64))[:, None] * np.ones((1, W))
+        assert np.array_equal(frames[f], expect.astype(np.float32)), f"frame {f}"
