@@ -20,6 +20,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_LIB_PATH") or os.path.join(HERE, "librtmi355x.so")  # override: A/B builds
 
 RT_OK, RT_DONE, RT_EBADARG, RT_ENODEV, RT_EHIP, RT_ENOMEM, RT_ETOOBIG = 0, 1, -1, -2, -3, -4, -5
+RT_ERANGE = -6
 RT_CAMERA, RT_POINT_LIGHT, RT_SPHERE, RT_TRIANGLE, RT_PLANE, RT_OTHER = range(6)
 RT_OUT_F64, RT_OUT_F32 = 0, 1
 RT_ORDER_EXACT, RT_ORDER_FAST = 0, 1
@@ -29,6 +30,7 @@ RT_MAX_DEPTH = 16
 EXPORTS = (
     "rt_abi_version", "rt_strerror", "rt_device_count", "rt_scene_check", "rt_scene_canon",
     "rt_render", "rt_prepare", "rt_shard_rows", "rt_launch", "rt_launch_spp", "rt_unshard", "rt_release",
+    "rt_ppm_bound", "rt_ppm_format", "rt_render_ppm_file",
 )
 
 
@@ -122,6 +124,10 @@ def lib() -> ctypes.CDLL:
     L.rt_shard_rows.argtypes = [u32, u32, u32]
     L.rt_launch.argtypes = [vp, u32, u32, u32, u32, u32, u32, i32, i32, vp, vp, vp]
     L.rt_launch_spp.argtypes = [vp, u32, u32, u32, u32, u32, u32, i32, i32, u32, ctypes.c_uint64, vp, vp, vp]
+    L.rt_ppm_bound.restype = ctypes.c_size_t
+    L.rt_ppm_bound.argtypes = [u32, u32, u32]
+    L.rt_ppm_format.argtypes = [vp, i32, u32, u32, u32, vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), vp]
+    L.rt_render_ppm_file.argtypes = [vp, u32, u32, u32, u32, vp, u32, ctypes.c_char_p, vp]
     L.rt_unshard.argtypes = [vp, u32, u32, u32, u32, i32, vp, vp]
     L.rt_release.argtypes = [vp]
     _LIB = L

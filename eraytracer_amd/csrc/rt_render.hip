@@ -924,7 +924,7 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
             }
         }
     }
-    if (!inside) return;
+    if (!active) return; // slab rows past the image are not written
     const size_t pix = (size_t)ly * W + x;
     if (PREC == RT_OUT_F64) {
         double *o = reinterpret_cast<double *>(out) + pix * 3;
@@ -1044,6 +1044,7 @@ const char *rt_strerror(int code) {
     case RT_EHIP: return "HIP runtime error";
     case RT_ENOMEM: return "out of memory";
     case RT_ETOOBIG: return "size exceeds a library limit";
+    case RT_ERANGE: return "a colour outside the device P3 formatter's range (below -2^31 after scaling)";
     default: return "unknown error";
     }
 }
@@ -1391,10 +1392,18 @@ int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dept
     int W = (int)width, H = (int)height, D = (int)depth, rb = (int)row_block, sh = (int)shard, ns = (int)nshards;
     const int slab_rows = (int)slab;
     if (spp > 1) { // RT_SUPERSAMPLING, on the wavefront engine: one pass per sample, summed in order
-        const size_t n = (size_t)slab_rows * W * 3;
-        int rc = grow(reinterpret_cast<void **>(&p->d_sample), &p->sample_bytes, 2 * n * sizeof(double), &p->gen);
+        // the slab rows inside the image (a prefix: global rows grow with slab rows)
+        size_t valid_rows = 0;
+        for (int blk = 0; blk * rb < slab_rows; ++blk) {
+            const long long base = ((long long)blk * ns + sh) * rb;
+            valid_rows += (size_t)std::max(0LL, std::min((long long)rb, (long long)H - base));
+        }
+        const size_t n = valid_rows * W * 3;
+        if (n == 0) return RT_OK;
+        const size_t n_slab = (size_t)slab_rows * W * 3;
+        int rc = grow(reinterpret_cast<void **>(&p->d_sample), &p->sample_bytes, 2 * n_slab * sizeof(double), &p->gen);
         if (rc != RT_OK) return rc;
-        double *smp = p->d_sample, *acc = p->d_sample + n;
+        double *smp = p->d_sample, *acc = p->d_sample + n_slab;
         const int blocks = (int)std::min<size_t>(8192, (n + 255) / 256);
         for (int s = 0; s < (int)spp; ++s) {
             rc = p->hdr.int_pow ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, slab_rows, smp,

@@ -148,8 +148,12 @@ def write_pixels_to_ppm(Width, Height, MaxValue, Pixels, Filename):
         f.write(f"{Width} {Height}\n")
         f.write(f"{MaxValue}\n")
         if isinstance(Pixels, np.ndarray):
-            q = np.minimum(np.trunc(Pixels.astype(np.float64).reshape(-1, 3) * MaxValue), MaxValue).astype(np.int64)
-            f.write("".join(f"{r} {g} {b} " for r, g, b in q.tolist()))
+            x = np.minimum(np.trunc(Pixels.astype(np.float64).reshape(-1, 3) * MaxValue), MaxValue)
+            if np.all(x > -2.0 ** 62):
+                rows = x.astype(np.int64).tolist()
+            else:  # BEAM integers are unbounded: exact Python ints for huge negative values
+                rows = [[int(v) for v in px] for px in x.tolist()]
+            f.write("".join(f"{r} {g} {b} " for r, g, b in rows))
         else:
             parts = []
             for _key, (r, g, b) in Pixels:
@@ -159,11 +163,48 @@ def write_pixels_to_ppm(Width, Height, MaxValue, Pixels, Filename):
 
 
 def raytrace(Width=4, Height=3, Filename="/tmp/traced.ppm", Recursion_depth=5, Function=None):
-    """raytrace/1,5 (raytracer.erl:721-733): render scene() with Function, write the PPM."""
+    """raytrace/1,5 (raytracer.erl:721-733): render scene() with Function, write the PPM.
+    The GPU strategy goes through rt_render_ppm_file (the P3 text is produced on the GPU,
+    byte-identical to write_pixels_to_ppm)."""
     if Function is None:
         Function = raytraced_pixel_list_gpu
+    if Function is raytraced_pixel_list_gpu:
+        return render_ppm_file(Width, Height, default_scene(), Recursion_depth, Filename)
     pixels = Function(Width, Height, default_scene(), Recursion_depth)
     return write_pixels_to_ppm(Width, Height, 255, pixels, Filename)
+
+
+def render_ppm_file(width: int, height: int, scene, depth: int, filename: str, *, max_value: int = 255,
+                    ndev: int = 1, first_dev: int = 0, spp: int = 1, seed: int = 0):
+    """Render and write the P3 file natively (rt_render_ppm_file): raytrace/5 + write_pixels_to_ppm/5."""
+    if not _sizes_ok(width, height):
+        return DONE
+    _depth_ok(depth)
+    elems = N.marshal(scene)
+    opts = N.RtOpts(ctypes.sizeof(N.RtOpts), first_dev, ndev, N.RT_OUT_F64, N.RT_ORDER_EXACT, 16, None, spp, 0, seed)
+    rc = N.lib().rt_render_ppm_file(elems, len(elems), width, height, depth, ctypes.byref(opts), max_value,
+                                    str(filename).encode(), None)
+    if rc == N.RT_DONE:
+        return DONE
+    N.check(rc, "rt_render_ppm_file")
+    return "ok"
+
+
+def ppm_text_gpu(img, max_value: int = 255) -> bytes:
+    """The P3 bytes of an (H, W, 3) frame formatted on the GPU (rt_ppm_format); RT_ERANGE
+    (a channel below -2^31 after scaling) raises."""
+    import torch
+    L = N.lib()
+    h, w, _ = img.shape
+    prec = N.RT_OUT_F64 if img.dtype == np.float64 else N.RT_OUT_F32
+    d = torch.from_numpy(np.ascontiguousarray(img)).cuda()
+    cap = L.rt_ppm_bound(w, h, max_value)
+    buf = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    n = ctypes.c_size_t(0)
+    st = torch.cuda.current_stream().cuda_stream
+    N.check(L.rt_ppm_format(d.data_ptr(), prec, w, h, max_value, buf.data_ptr(), cap, ctypes.byref(n), st),
+            "rt_ppm_format")
+    return bytes(buf[: n.value].cpu().numpy())
 
 
 def go(Strategy, Width=None, Height=None, Filename=None, Recursion_depth=None):

@@ -47,6 +47,7 @@ extern "C" {
 #define RT_EHIP (-3)       /* a HIP runtime call failed */
 #define RT_ENOMEM (-4)     /* host or device allocation failed */
 #define RT_ETOOBIG (-5)    /* size exceeds a documented limit (see RT_MAX_*) */
+#define RT_ERANGE (-6)     /* rt_ppm_format: a channel below -2^31 after scaling (see there) */
 
 #define RT_MAX_DEPTH 16    /* recursion depths above this are rejected */
 #define RT_MAX_OBJECTS 4096
@@ -161,7 +162,8 @@ int rt_render(const rt_elem *scene, uint32_t n_elems, uint32_t width, uint32_t h
  * in interleaved blocks of `row_block` rows: global row g belongs to shard
  * (g / row_block) % nshards.  d_out receives the shard's rows packed in order,
  * rt_shard_rows(height,row_block,nshards) rows of width*3 elements; slab rows past
- * the image are written as zero.  d_levels (optional) gets one byte per slab pixel. */
+ * the image (the tail of the last row block) are not written, so with nshards = 1 a buffer
+ * of `height` rows suffices.  d_levels (optional) gets one byte per slab pixel. */
 typedef struct rt_prepared rt_prepared;
 
 int rt_prepare(const rt_elem *scene, uint32_t n_elems, int device, rt_prepared **out);
@@ -178,6 +180,26 @@ int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dept
 int rt_unshard(const void *d_slabs, uint32_t width, uint32_t height, uint32_t row_block,
                uint32_t nshards, int precision, void *d_image, void *stream);
 int rt_release(rt_prepared *p);
+
+/* ---- P3 output: write_pixels_to_ppm/5 (raytracer.erl:667-685) -----------------------
+ * The file is "P3\nW H\nMaxValue\n" followed, for every pixel in row order, by
+ * "R G B " where each channel is min(trunc(C*MaxValue), MaxValue) printed in decimal
+ * (C*MaxValue in binary64; no lower clamp, so a negative colour prints a negative
+ * number).  Byte-exact for RT_OUT_F64 frames; an RT_OUT_F32 frame is formatted from its
+ * float values.
+ * rt_ppm_bound: a byte count that always suffices for rt_ppm_format's output.
+ * rt_ppm_format: formats a device frame (precision as rt_launch writes it) into the device
+ *   buffer d_text (text_cap bytes) on `stream`, then synchronises it to report *text_len.
+ *   RT_ERANGE if a channel is below -2^31 (BEAM prints such values as bignums; the file
+ *   API below formats them on the host), RT_ETOOBIG if text_cap is too small.
+ * rt_render_ppm_file: raytrace/5 without the strategy fun — render (opts as rt_render) and
+ *   write the P3 file at `path`; the text is produced on the GPU. */
+size_t rt_ppm_bound(uint32_t width, uint32_t height, uint32_t max_value);
+int rt_ppm_format(const void *d_rgb, int precision, uint32_t width, uint32_t height, uint32_t max_value,
+                  char *d_text, size_t text_cap, size_t *text_len, void *stream);
+int rt_render_ppm_file(const rt_elem *scene, uint32_t n_elems, uint32_t width, uint32_t height,
+                       uint32_t depth, const rt_opts *opts, uint32_t max_value, const char *path,
+                       rt_stats *stats);
 
 #ifdef __cplusplus
 }

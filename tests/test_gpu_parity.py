@@ -233,3 +233,92 @@ def test_supersampling_shards():
                                st) == N.RT_EBADARG
     finally:
         L.rt_release(p)
+
+
+# ---- P3 output on the GPU (write_pixels_to_ppm/5, raytracer.erl:667-685) ---------------------
+
+def _py_ppm(tmp_path, img, maxv=255):
+    from eraytracer_amd.raytracer import write_pixels_to_ppm
+    path = tmp_path / "py.ppm"
+    write_pixels_to_ppm(img.shape[1], img.shape[0], maxv, img, str(path))
+    return path.read_bytes()
+
+
+def test_ppm_gpu_bytes_match_python_writer(tmp_path):
+    """rt_ppm_format's text equals the Python mirror of write_pixels_to_ppm/5 byte for byte:
+    rendered frames (incl. negative colours) and adversarial values (exact k/255 and
+    half-step boundaries, clamping, negatives, zero)."""
+    from eraytracer_amd.raytracer import ppm_text_gpu
+    from tests.test_oracle import TRICKY
+    frames = [render(64, 48, records.scene(), 5), render(40, 30, TRICKY[5](), 3),
+              render(48, 40, scenes.s64(), 5, spp=3, seed=9)]
+    k = np.arange(0, 600, dtype=np.float64)
+    vals = np.concatenate([k / 255.0, (k + 0.5) / 255.0, -k / 255.0, np.nextafter(k / 255.0, -1.0),
+                           [0.0, -0.0, 1.0, 2.0, 1e30, -1e5, 254.999999999 / 255.0, 1.0 - 1e-17]])
+    vals = np.resize(vals, (len(vals) + 2) // 3 * 3).reshape(-1, 3)
+    frames.append(vals.reshape(1, -1, 3))
+    for img in frames:
+        assert ppm_text_gpu(img) == _py_ppm(tmp_path, img)
+    for maxv in (1, 7, 65535):
+        assert ppm_text_gpu(frames[0], maxv) == _py_ppm(tmp_path, frames[0], maxv)
+
+
+def test_ppm_gpu_range_error():
+    from eraytracer_amd.raytracer import ppm_text_gpu
+    img = np.zeros((2, 3, 3))
+    img[1, 2, 0] = -1e12  # -2.55e14 after scaling: BEAM prints a bignum
+    with pytest.raises(N.RtError):
+        ppm_text_gpu(img)
+
+
+def test_render_ppm_file_matches_golden_and_python(tmp_path, oracle):
+    """rt_render_ppm_file (raytrace/5 with the P3 text made on the GPU) reproduces the
+    committed run.sh / run-concurrent.sh P3 fixtures and the Python writer on the oracle's
+    frame — including a scene whose colours need BEAM bignums (host formatting path)."""
+    import os
+    from eraytracer_amd.raytracer import render_ppm_file
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    for name, w, h in (("run_sh_32x24_d1.ppm", 32, 24), ("run_concurrent_sh_16x12_d1.ppm", 16, 12)):
+        out = tmp_path / name
+        assert render_ppm_file(w, h, records.scene(), 1, str(out)) == "ok"
+        assert out.read_bytes() == open(os.path.join(gold, name), "rb").read()
+    sc = scenes.s64()
+    out = tmp_path / "s64.ppm"
+    render_ppm_file(56, 40, sc, 5, str(out))
+    ref = _oracle(oracle, sc, 56, 40, 5)[0]
+    got, want = out.read_bytes(), _py_ppm(tmp_path, ref)
+    if got != want:
+        ta, tb = got.split(b"\n", 3)[3].split(), want.split(b"\n", 3)[3].split()
+        diff = [(k // 3 // 56, k // 3 % 56, k % 3, ta[k], tb[k], repr(ref.reshape(-1)[k]))
+                for k in range(min(len(ta), len(tb))) if ta[k] != tb[k]]
+        raise AssertionError(f"{len(got)} vs {len(want)} bytes; {len(diff)} values differ: {diff[:6]}")
+    huge = records.scene()[:2] + [records.sphere(4, records.vector(4, 0, 10),
+                                                 records.material(records.colour(-1e12, 0.5, 1), 20, 1, 0.1))]
+    out = tmp_path / "huge.ppm"
+    render_ppm_file(24, 18, huge, 3, str(out))
+    assert out.read_bytes() == _py_ppm(tmp_path, _oracle(oracle, huge, 24, 18, 3)[0])
+    assert b"-" in out.read_bytes()
+
+
+@pytest.mark.parametrize("name,spp", [("s64", 1), ("s64", 3), ("default", 1)])
+def test_launch_writes_only_image_rows(name, spp):
+    """A single-shard launch touches only the image's rows: H not a multiple of the row
+    block, the output followed by guard rows that must keep their sentinel (an earlier
+    version wrote the last block's padding rows past the buffer)."""
+    import torch
+    L = N.lib()
+    el = N.marshal(scenes.named(name))
+    w, h, rb = 40, 37, 16
+    p = ctypes.c_void_p()
+    N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(p)), "rt_prepare")
+    try:
+        st = torch.cuda.current_stream().cuda_stream
+        buf = torch.full((h + 16, w, 3), 12345.0, dtype=torch.float64, device="cuda")
+        lv = torch.full((h + 16, w), 77, dtype=torch.uint8, device="cuda")
+        N.check(L.rt_launch_spp(p, w, h, 5, rb, 0, 1, N.RT_OUT_F64, N.RT_ORDER_EXACT, spp, 5, buf.data_ptr(),
+                                lv.data_ptr(), st))
+        torch.cuda.synchronize()
+        assert bool((buf[h:] == 12345.0).all()) and bool((lv[h:] == 77).all())
+        assert not bool((buf[:h] == 12345.0).any())
+    finally:
+        L.rt_release(p)
