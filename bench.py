@@ -257,6 +257,19 @@ def main():
                        seed=args.seed)
                 ts.append(st["total_ms"])
             line["boundary_mpx_s"] = round(frame_px / (min(ts) / 1e3) / 1e6, 3)
+            # raytrace/5 end to end natively: render + P3 text on the GPU + file write
+            # (write_pixels_to_ppm/5, byte-exact); the binary64 frame never leaves the GPU
+            import tempfile
+            from eraytracer_amd.raytracer import render_ppm_file
+            with tempfile.TemporaryDirectory() as td:
+                path = os.path.join(td, "frame.ppm")
+                tp = []
+                for _ in range(2):
+                    t1 = time.perf_counter()
+                    render_ppm_file(W, H, scene, args.depth, path, spp=args.spp, seed=args.seed)
+                    tp.append(time.perf_counter() - t1)
+                line["p3_file_mpx_s"] = round(frame_px / min(tp) / 1e6, 3)
+                line["p3_file_bytes"] = os.path.getsize(path)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, W, H, args.depth, args.cpu_seconds, args.spp, args.seed)
         print(json.dumps(line), flush=True)

@@ -240,10 +240,35 @@ static ERL_NIF_TERM render_binary_nif(ErlNifEnv *env, int argc, const ERL_NIF_TE
     return enif_make_binary(env, &bin);
 }
 
+/* render_ppm_file(W, H, Scene, Depth, Filename) -> ok | done: raytrace/5's render and
+ * write_pixels_to_ppm/5 (MaxValue 255) in one call; the P3 text is made on the GPU. */
+static ERL_NIF_TERM render_ppm_file_nif(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    unsigned W, H, D, n = 0;
+    char path[4096];
+    rt_elem *elems = NULL;
+    ERL_NIF_TERM *terms = NULL, ret;
+    (void)argc;
+    if (!enif_get_uint(env, argv[0], &W) || !enif_get_uint(env, argv[1], &H) || !enif_get_uint(env, argv[3], &D))
+        return enif_make_badarg(env);
+    if (enif_get_string(env, argv[4], path, sizeof path, ERL_NIF_LATIN1) <= 0) return enif_make_badarg(env);
+    if (W == 0 && H == 0) return atom_done;
+    if (W == 0 || H == 0) return enif_make_badarg(env);
+    if (!marshal_scene(env, argv[2], &elems, &terms, &n)) {
+        ret = enif_make_badarg(env);
+    } else {
+        int rc = rt_render_ppm_file(elems, n, W, H, D, NULL, 255, path, NULL);
+        ret = rc == RT_OK ? enif_make_atom(env, "ok") : rt_error(env, rc);
+    }
+    if (elems) enif_free(elems);
+    if (terms) enif_free(terms);
+    return ret;
+}
+
 static ErlNifFunc funcs[] = {
     {"render", 5, render_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"render_binary", 4, render_binary_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"render_binary", 5, render_binary_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"render_ppm_file", 5, render_ppm_file_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
 };
 
 ERL_NIF_INIT(rt_nif, funcs, load, NULL, NULL, NULL)

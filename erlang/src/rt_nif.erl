@@ -1,6 +1,6 @@
 %% rt_nif.erl — Erlang side of the NIF in erlang/c_src/rt_nif.c.
 -module(rt_nif).
--export([render/5, render_binary/4, render_binary/5]).
+-export([render/5, render_binary/4, render_binary/5, render_ppm_file/5]).
 -on_load(init/0).
 
 init() ->
@@ -21,4 +21,9 @@ render_binary(_Width, _Height, _Scene, _Depth) ->
 %% render_binary(Width, Height, Scene, Depth, #{spp => N, seed => S}) -> done | binary()
 %% Stochastic supersampling as defined at RT_SUPERSAMPLING in include/rt_mi355x.h.
 render_binary(_Width, _Height, _Scene, _Depth, _Opts) ->
+    erlang:nif_error(nif_not_loaded).
+
+%% render_ppm_file(Width, Height, Scene, Depth, Filename) -> ok | done
+%% raytrace/5's render plus write_pixels_to_ppm/5 (MaxValue 255), the P3 text made on the GPU.
+render_ppm_file(_Width, _Height, _Scene, _Depth, _Filename) ->
     erlang:nif_error(nif_not_loaded).
