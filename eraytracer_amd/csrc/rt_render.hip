@@ -951,7 +951,9 @@ struct rt_prepared {
     // wavefront-engine work space, grown on demand (one rt_launch in flight per rt_prepared)
     void *d_queue = nullptr;  // HitRec[slab pixels * depth]
     size_t queue_bytes = 0;
-    double *d_colbuf = nullptr; // colours of levels 1 .. depth-1, 3 doubles per slot
+    double *d_colbuf = nullptr; // colours of level 1, 3 doubles per slot
+    uint8_t *d_child = nullptr; // per level and slot: the record's reflection hit something
+    size_t child_bytes = 0;
     double *d_sample = nullptr; // supersampling: one sample's slab and the running sum
     size_t sample_bytes = 0;
     size_t colbuf_bytes = 0;
@@ -1108,6 +1110,7 @@ int rt_release(rt_prepared *p) {
     (void)hipFree(p->d_itab);
     if (p->d_queue) (void)hipFree(p->d_queue);
     if (p->d_colbuf) (void)hipFree(p->d_colbuf);
+    if (p->d_child) (void)hipFree(p->d_child);
     if (p->d_sample) (void)hipFree(p->d_sample);
     if (p->d_counts) (void)hipFree(p->d_counts);
     if (p->d_items) (void)hipFree(p->d_items);
@@ -1183,10 +1186,12 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     const size_t max_tiles = (size_t)tiles_x * ((pass_rows + TILE - 1) / TILE);
     const size_t slots = max_tiles * TILE_SLOTS; // per level
     int rc = grow(&p->d_queue, &p->queue_bytes, slots * nlev * sizeof(HitRec), &p->gen);
-    // colours of levels 1 .. depth-1, 3 doubles per slot (level 0 goes straight to the frame)
-    const size_t col_doubles = slots * 3 * (size_t)std::max(1, nlev - 1);
+    // colours of level 1, 3 doubles per slot (level 0 goes straight to the frame; deeper
+    // levels are shaded inside the chain walk), and per level the has-a-child flags
+    const size_t col_doubles = slots * 3;
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_colbuf), &p->colbuf_bytes, col_doubles * sizeof(double), &p->gen);
+    if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_child), &p->child_bytes, slots * nlev, &p->gen);
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_counts), &p->counts_bytes, max_tiles * nlev * sizeof(int), &p->gen);
     // dense work lists: 64 per-level record counts, then per level the slots of its records
@@ -1216,7 +1221,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         auto ck = [&](int k) { return p->d_counts + (size_t)k * ntiles; };
         int *nitems = p->d_items; // [0, 64): per-level record counts
         auto ik = [&](int k) { return p->d_items + 64 + (size_t)k * ntiles * TILE_SLOTS; };
-        auto colk = [&](int k) { return k > 0 ? p->d_colbuf + (size_t)(k - 1) * ntiles * TILE_SLOTS * 3 : nullptr; };
+        auto colk = [&](int k) { return k == 1 ? p->d_colbuf : nullptr; };
+        auto chk = [&](int k) { return p->d_child + (size_t)k * ntiles * TILE_SLOTS; };
         HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
         dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
@@ -1228,11 +1234,13 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                                D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed);
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
-        // level k's dense list, then its shading (k_light reads only level k: on the side stream
-        // it starts as soon as the list exists and runs beside the next reflections)
+        // level k's dense list, then for levels 0 and 1 their shading (k_light reads only level k:
+        // on a side stream it starts as soon as the list exists and runs beside the next
+        // reflections); deeper levels are shaded by the chain walk
         auto level_lists = [&](int k) -> int {
             hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k);
             HIPCHK(hipGetLastError());
+            if (k > 1) return RT_OK;
             if (overlap) {
                 HIPCHK(hipEventRecord(p->ev_level[k], st));
                 HIPCHK(hipStreamWaitEvent(ls(k), p->ev_level[k], 0));
@@ -1253,32 +1261,38 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             // waves each, bound by one wave's dependent chain: they walk two candidates per step
             if (lv && k == 1)
                 hipLaunchKernelGGL((k_reflect<true, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1));
             else if (lv)
                 hipLaunchKernelGGL((k_reflect<true, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1));
             else if (k == 1)
                 hipLaunchKernelGGL((k_reflect<false, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1));
             else
                 hipLaunchKernelGGL((k_reflect<false, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv);
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1));
             HIPCHK(hipGetLastError());
             if ((rc = level_lists(k)) != RT_OK) return rc;
         }
-        // reshading level k reads level k+1's final colours and level k's shadow answers: it
-        // waits for those two levels' shading only (level 0's, the longest, joins last)
-        if (overlap && nrefl > 0) HIPCHK(hipStreamWaitEvent(st, p->ev_lit[nrefl], 0));
-        if (overlap && nrefl == 0 && nshade > 0) HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
-        for (int k = nrefl - 1; k >= 0; --k) {
-            if (overlap) HIPCHK(hipStreamWaitEvent(st, p->ev_lit[k], 0));
-            if (p->hdr.n_light <= 32) // the shadow answers fit the record
-                hipLaunchKernelGGL((k_back<PREC, GENPOW, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                                   p->d_itab, k, o, qk(k), qk(k + 1), ik(k + 1), nitems + (k + 1), colk(k + 1), colk(k));
-            else
-                hipLaunchKernelGGL((k_back<PREC, GENPOW, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                                   p->d_itab, k, o, qk(k), qk(k + 1), ik(k + 1), nitems + (k + 1), colk(k + 1), colk(k));
+        // the chain walk reads the colours and shadow bits of levels 0 and 1
+        if (nrefl > 0) {
+            if (overlap) {
+                HIPCHK(hipStreamWaitEvent(st, p->ev_lit[1], 0));
+                HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
+            }
+            const size_t ls_ = (size_t)ntiles * TILE_SLOTS;
+            const bool bits = p->hdr.n_light <= 32; // the shadow answers fit the record
+#define RT_WALK(SPHV, BITSV)                                                                                        \
+    hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,    \
+                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child)
+            if (sph_only && bits) RT_WALK(true, true);
+            else if (sph_only) RT_WALK(true, false);
+            else if (bits) RT_WALK(false, true);
+            else RT_WALK(false, false);
+#undef RT_WALK
             HIPCHK(hipGetLastError());
+        } else if (overlap && nshade > 0) {
+            HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
         }
     }
     return RT_OK;
