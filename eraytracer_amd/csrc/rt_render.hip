@@ -951,7 +951,7 @@ struct rt_prepared {
     // wavefront-engine work space, grown on demand (one rt_launch in flight per rt_prepared)
     void *d_queue = nullptr;  // HitRec[slab pixels * depth]
     size_t queue_bytes = 0;
-    double *d_colbuf = nullptr; // colours of level 1, 3 doubles per slot
+    double *d_colbuf = nullptr; // colours of levels 1 and 2, 3 doubles per slot each
     uint8_t *d_child = nullptr; // per level and slot: the record's reflection hit something
     size_t child_bytes = 0;
     double *d_sample = nullptr; // supersampling: one sample's slab and the running sum
@@ -1188,7 +1188,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     int rc = grow(&p->d_queue, &p->queue_bytes, slots * nlev * sizeof(HitRec), &p->gen);
     // colours of level 1, 3 doubles per slot (level 0 goes straight to the frame; deeper
     // levels are shaded inside the chain walk), and per level the has-a-child flags
-    const size_t col_doubles = slots * 3;
+    const size_t col_doubles = slots * 3 * 2;
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_colbuf), &p->colbuf_bytes, col_doubles * sizeof(double), &p->gen);
     if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_child), &p->child_bytes, slots * nlev, &p->gen);
@@ -1274,17 +1274,28 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             HIPCHK(hipGetLastError());
             if ((rc = level_lists(k)) != RT_OK) return rc;
         }
-        // the chain walk reads the colours and shadow bits of levels 0 and 1
+        // the chain walk: phase A (levels >= 2) needs only the chain, phase B the shading of
+        // levels 0 and 1 too
         if (nrefl > 0) {
+            const size_t ls_ = (size_t)ntiles * TILE_SLOTS;
+            double *col1 = p->d_colbuf, *col2 = p->d_colbuf + ls_ * 3;
+            if (D > 2) {
+                if (sph_only)
+                    hipLaunchKernelGGL((k_walk_deep<GENPOW, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
+                                       p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, col2);
+                else
+                    hipLaunchKernelGGL((k_walk_deep<GENPOW, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
+                                       p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, col2);
+                HIPCHK(hipGetLastError());
+            }
             if (overlap) {
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[1], 0));
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
             }
-            const size_t ls_ = (size_t)ntiles * TILE_SLOTS;
             const bool bits = p->hdr.n_light <= 32; // the shadow answers fit the record
 #define RT_WALK(SPHV, BITSV)                                                                                        \
     hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,    \
-                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child)
+                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, col1, col2, p->d_child)
             if (sph_only && bits) RT_WALK(true, true);
             else if (sph_only) RT_WALK(true, false);
             else if (bits) RT_WALK(false, true);
