@@ -951,7 +951,7 @@ struct rt_prepared {
     // wavefront-engine work space, grown on demand (one rt_launch in flight per rt_prepared)
     void *d_queue = nullptr;  // HitRec[slab pixels * depth]
     size_t queue_bytes = 0;
-    double *d_colbuf = nullptr; // colours of levels 1 and 2, 3 doubles per slot each
+    double *d_colbuf = nullptr; // colours of levels 1 .. depth-1, 3 doubles per slot
     uint8_t *d_child = nullptr; // per level and slot: the record's reflection hit something
     size_t child_bytes = 0;
     double *d_sample = nullptr; // supersampling: one sample's slab and the running sum
@@ -1186,9 +1186,9 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     const size_t max_tiles = (size_t)tiles_x * ((pass_rows + TILE - 1) / TILE);
     const size_t slots = max_tiles * TILE_SLOTS; // per level
     int rc = grow(&p->d_queue, &p->queue_bytes, slots * nlev * sizeof(HitRec), &p->gen);
-    // colours of level 1, 3 doubles per slot (level 0 goes straight to the frame; deeper
-    // levels are shaded inside the chain walk), and per level the has-a-child flags
-    const size_t col_doubles = slots * 3 * 2;
+    // colours of levels 1 .. depth-1, 3 doubles per slot (level 0 goes straight to the
+    // frame), and per level the has-a-child flags
+    const size_t col_doubles = slots * 3 * (size_t)std::max(1, nlev - 1);
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_colbuf), &p->colbuf_bytes, col_doubles * sizeof(double), &p->gen);
     if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_child), &p->child_bytes, slots * nlev, &p->gen);
@@ -1221,7 +1221,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         auto ck = [&](int k) { return p->d_counts + (size_t)k * ntiles; };
         int *nitems = p->d_items; // [0, 64): per-level record counts
         auto ik = [&](int k) { return p->d_items + 64 + (size_t)k * ntiles * TILE_SLOTS; };
-        auto colk = [&](int k) { return k == 1 ? p->d_colbuf : nullptr; };
+        auto colk = [&](int k) { return k > 0 ? p->d_colbuf + (size_t)(k - 1) * ntiles * TILE_SLOTS * 3 : nullptr; };
         auto chk = [&](int k) { return p->d_child + (size_t)k * ntiles * TILE_SLOTS; };
         HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
@@ -1234,13 +1234,11 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                                D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed);
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
-        // level k's dense list, then for levels 0 and 1 their shading (k_light reads only level k:
-        // on a side stream it starts as soon as the list exists and runs beside the next
-        // reflections); deeper levels are shaded by the chain walk
+        // level k's dense list, then its shading (k_light reads only level k: on a side stream
+        // it starts as soon as the list exists and runs beside the next reflections)
         auto level_lists = [&](int k) -> int {
             hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k);
             HIPCHK(hipGetLastError());
-            if (k > 1) return RT_OK;
             if (overlap) {
                 HIPCHK(hipEventRecord(p->ev_level[k], st));
                 HIPCHK(hipStreamWaitEvent(ls(k), p->ev_level[k], 0));
@@ -1274,28 +1272,28 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             HIPCHK(hipGetLastError());
             if ((rc = level_lists(k)) != RT_OK) return rc;
         }
-        // the chain walk: phase A (levels >= 2) needs only the chain, phase B the shading of
-        // levels 0 and 1 too
+        // deep levels (see deep_dense): k_walk_deep right after the chain, then k_walk once
+        // every level's shading is in (side stream 1 shades levels 1.. in order: its last
+        // level's event covers them all)
         if (nrefl > 0) {
             const size_t ls_ = (size_t)ntiles * TILE_SLOTS;
-            double *col1 = p->d_colbuf, *col2 = p->d_colbuf + ls_ * 3;
             if (D > 2) {
                 if (sph_only)
                     hipLaunchKernelGGL((k_walk_deep<GENPOW, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
-                                       p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, col2);
+                                       p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, colk(2));
                 else
                     hipLaunchKernelGGL((k_walk_deep<GENPOW, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
-                                       p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, col2);
+                                       p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, colk(2));
                 HIPCHK(hipGetLastError());
             }
             if (overlap) {
-                HIPCHK(hipStreamWaitEvent(st, p->ev_lit[1], 0));
+                HIPCHK(hipStreamWaitEvent(st, p->ev_lit[nrefl], 0));
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
             }
             const bool bits = p->hdr.n_light <= 32; // the shadow answers fit the record
 #define RT_WALK(SPHV, BITSV)                                                                                        \
     hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,    \
-                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, col1, col2, p->d_child)
+                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child)
             if (sph_only && bits) RT_WALK(true, true);
             else if (sph_only) RT_WALK(true, false);
             else if (bits) RT_WALK(false, true);
