@@ -1272,11 +1272,31 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             HIPCHK(hipGetLastError());
             if ((rc = level_lists(k)) != RT_OK) return rc;
         }
-        // deep levels (see deep_dense): k_walk_deep right after the chain, then k_walk once
-        // every level's shading is in (side stream 1 shades levels 1.. in order: its last
-        // level's event covers them all)
+        // deep levels (see deep_dense): k_walk_deep right after the chain; the chains ending at
+        // level 1 (the bulk) are finished on side stream 0 as soon as levels 0 and 1 are
+        // shaded, beside it; then the rest, once every level's shading is in (side stream 1
+        // shades levels 1.. in order: its last level's event covers them all)
         if (nrefl > 0) {
             const size_t ls_ = (size_t)ntiles * TILE_SLOTS;
+            const bool bits = p->hdr.n_light <= 32; // the shadow answers fit the record
+            auto walk = [&](hipStream_t s_, int lo, int hi) {
+#define RT_WALK(SPHV, BITSV)                                                                                        \
+    hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV>), dim3(sblocks), dim3(BLOCK), 0, s_, p->hdr, p->d_tab,    \
+                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child, lo, hi)
+                if (sph_only && bits) RT_WALK(true, true);
+                else if (sph_only) RT_WALK(true, false);
+                else if (bits) RT_WALK(false, true);
+                else RT_WALK(false, false);
+#undef RT_WALK
+            };
+            if (overlap) { // side stream 0 (after level 0's shading) waits for level 1's, and for
+                           // k_reflect(2), which marks the level-1 records that have a child
+                HIPCHK(hipStreamWaitEvent(p->side[0], p->ev_lit[1], 0));
+                if (D > 2) HIPCHK(hipStreamWaitEvent(p->side[0], p->ev_level[2], 0));
+                walk(p->side[0], 1, 2);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipEventRecord(p->ev_lit[0], p->side[0]));
+            }
             if (D > 2) {
                 if (sph_only)
                     hipLaunchKernelGGL((k_walk_deep<GENPOW, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
@@ -1289,16 +1309,10 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             if (overlap) {
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[nrefl], 0));
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
+            } else {
+                walk(st, 1, 2);
             }
-            const bool bits = p->hdr.n_light <= 32; // the shadow answers fit the record
-#define RT_WALK(SPHV, BITSV)                                                                                        \
-    hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,    \
-                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child)
-            if (sph_only && bits) RT_WALK(true, true);
-            else if (sph_only) RT_WALK(true, false);
-            else if (bits) RT_WALK(false, true);
-            else RT_WALK(false, false);
-#undef RT_WALK
+            if (D > 2) walk(st, 2, D);
             HIPCHK(hipGetLastError());
         } else if (overlap && nshade > 0) {
             HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
