@@ -954,6 +954,8 @@ struct rt_prepared {
     double *d_colbuf = nullptr; // colours of levels 1 .. depth-1, 3 doubles per slot
     uint8_t *d_child = nullptr; // per level and slot: the record's reflection hit something
     size_t child_bytes = 0;
+    unsigned *d_lit = nullptr;  // per level and slot: shadow answers of lights 0..31 (k_light)
+    size_t lit_bytes = 0;
     double *d_sample = nullptr; // supersampling: one sample's slab and the running sum
     size_t sample_bytes = 0;
     size_t colbuf_bytes = 0;
@@ -1111,6 +1113,7 @@ int rt_release(rt_prepared *p) {
     if (p->d_queue) (void)hipFree(p->d_queue);
     if (p->d_colbuf) (void)hipFree(p->d_colbuf);
     if (p->d_child) (void)hipFree(p->d_child);
+    if (p->d_lit) (void)hipFree(p->d_lit);
     if (p->d_sample) (void)hipFree(p->d_sample);
     if (p->d_counts) (void)hipFree(p->d_counts);
     if (p->d_items) (void)hipFree(p->d_items);
@@ -1193,6 +1196,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         rc = grow(reinterpret_cast<void **>(&p->d_colbuf), &p->colbuf_bytes, col_doubles * sizeof(double), &p->gen);
     if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_child), &p->child_bytes, slots * nlev, &p->gen);
     if (rc == RT_OK)
+        rc = grow(reinterpret_cast<void **>(&p->d_lit), &p->lit_bytes, slots * nlev * sizeof(unsigned), &p->gen);
+    if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_counts), &p->counts_bytes, max_tiles * nlev * sizeof(int), &p->gen);
     // dense work lists: 64 per-level record counts, then per level the slots of its records
     const size_t items_ints = slots * nlev + 64;
@@ -1223,6 +1228,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         auto ik = [&](int k) { return p->d_items + 64 + (size_t)k * ntiles * TILE_SLOTS; };
         auto colk = [&](int k) { return k > 0 ? p->d_colbuf + (size_t)(k - 1) * ntiles * TILE_SLOTS * 3 : nullptr; };
         auto chk = [&](int k) { return p->d_child + (size_t)k * ntiles * TILE_SLOTS; };
+        auto litk = [&](int k) { return p->d_lit + (size_t)k * ntiles * TILE_SLOTS; };
         HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
         dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
@@ -1245,10 +1251,10 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             }
             if (sph_only)
                 hipLaunchKernelGGL((k_light<PREC, GENPOW, true>), dim3(sblocks), dim3(BLOCK), 0, ls(k), p->hdr,
-                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k));
+                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k));
             else
                 hipLaunchKernelGGL((k_light<PREC, GENPOW, false>), dim3(sblocks), dim3(BLOCK), 0, ls(k), p->hdr,
-                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k));
+                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k));
             HIPCHK(hipGetLastError());
             if (overlap) HIPCHK(hipEventRecord(p->ev_lit[k], ls(k)));
             return RT_OK;
@@ -1282,7 +1288,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             auto walk = [&](hipStream_t s_, int lo, int hi) {
 #define RT_WALK(SPHV, BITSV)                                                                                        \
     hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV>), dim3(sblocks), dim3(BLOCK), 0, s_, p->hdr, p->d_tab,    \
-                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child, lo, hi)
+                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child, p->d_lit, lo, hi)
                 if (sph_only && bits) RT_WALK(true, true);
                 else if (sph_only) RT_WALK(true, false);
                 else if (bits) RT_WALK(false, true);
