@@ -3,7 +3,7 @@ set -o pipefail
 TAG=${1:-run}; shift || true
 mkdir -p gpurun_out
 make -C oracle > /dev/null
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_$TAG.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_$TAG.log; exit 1; }
 tail -2 gpurun_out/pytest_$TAG.log
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline "$@" > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
