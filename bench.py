@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-boundary", action="store_true")
+    ap.add_argument("--gather", default="compact", choices=["compact", "dense"],
+                    help="N > 1: compact = background pixels not sent (rt_slab_pack, default); dense = whole slabs")
     return ap.parse_args()
 
 
@@ -145,20 +147,26 @@ def main():
     # With N > 1 ranks a step is render + gather to rank 0 + reorder; frames are pipelined
     # (frame i+1 renders while frame i's gather is in flight, dist.SlabPipeline) and the
     # timed region ends only when every frame is gathered and reordered.
-    pipe = fr.pipeline() if world > 1 else None
+    # The compact gather (default) sends only the non-background pixels: rank 0's inbound xGMI
+    # links, not the render, bound a frame at N = 8 (dist.CompactGather).
+    pipe = None
+    if world > 1:
+        pipe = fr.compact_gather() if args.gather == "compact" else fr.pipeline()
 
     def one_step(e0=None, e1=None):
-        if pipe is not None:
+        if pipe is not None and args.gather == "dense":
             fr.slab = pipe.slab
         if e0 is not None:
             e0.record()
         fr.launch()
         if e1 is not None:
             e1.record()
-        if pipe is not None:
-            pipe.submit()
-        else:
+        if pipe is None:
             fr.gather()
+        elif args.gather == "compact":
+            pipe.submit(fr.slab, rank)
+        else:
+            pipe.submit()
 
     for _ in range(args.warmup):
         one_step()
@@ -224,7 +232,7 @@ def main():
                        + (f" x{args.spp} spp" if args.spp > 1 else ""), "scene": args.scene, "spp": args.spp,
                        "width": W, "height": H, "depth": args.depth, "order": args.order,
                        "framebuffer": args.precision, "row_block": args.row_block,
-                       "parallelism": f"rows{world}" + ("+rccl_gather" if world > 1 else ""),
+                       "parallelism": f"rows{world}" + (f"+rccl_{args.gather}_gather" if world > 1 else ""),
                        "spheres": counts["spheres"], "triangles": counts["triangles"], "planes": counts["planes"],
                        "lights": counts["lights"]},
             "roofline": {"bound": "valu", "achieved": round(valu_ach, 3), "peak": PEAK_FP64_VALU_TOPS,

@@ -1,0 +1,240 @@
+// rt_slab.hip — compact slabs for the multi-GPU frame gather (include/rt_mi355x.h, "compact
+// slab transfer").
+//
+// The reference's master collects every pixel from its workers (raytracer.erl:151-161,
+// :169-178); here each rank renders its interleaved rows into a slab in HBM and rank 0
+// gathers the slabs over xGMI.  Rendering runs at ~22 Gpx/s per MI355X, i.e. ~260 GB/s of
+// f32 RGB per GPU, so with 8 ranks the gather into rank 0 (7 inbound links) and not the
+// render bounds a frame.  Most pixels are background (the reference's BACKGROUND_COLOUR,
+// raytracer.erl:186-203, exactly +0.0 in every channel: 73 % of S64's pixels), so a slab
+// is sent as
+//     header (fixed size):  u64 count | u32 block_off[nblk] | u64 mask[4*nblk]
+//     values (count*3 elements of the slab's precision): the non-zero pixels in slab order
+// with one mask bit per slab pixel (a pixel is "zero" iff all three channels are +0.0
+// bit for bit, so the round trip is exact) and, per 256-pixel block, the number of
+// non-zero pixels before it.  Slab rows past the image are never written by rt_launch and
+// are encoded as zero without being read.
+//
+// Pack: k_mask (one wave per 64 pixels: ballot -> mask word, block popcount), k_scan (one
+// workgroup, exclusive scan of the block counts -> offsets and the count), k_compact
+// (non-zero pixels copied to their rank).  Unpack on rank 0 is fused with the reorder of
+// rt_unshard: one thread per image pixel finds its shard, slab pixel and mask bit and
+// reads its value, so the full frame is written once.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/rt_mi355x.h"
+
+namespace {
+
+constexpr int SLAB_BLOCK = 256;       // pixels per offset entry = threads per pack workgroup
+constexpr size_t HDR_OFFS = 64;       // block offsets start here (the count sits at 0)
+
+#define SLABCHK(x)                                                                                                 \
+    do {                                                                                                           \
+        hipError_t e_ = (x);                                                                                       \
+        if (e_ != hipSuccess) {                                                                                    \
+            std::fprintf(stderr, "rt_mi355x: %s failed: %s\n", #x, hipGetErrorString(e_));                        \
+            return RT_EHIP;                                                                                        \
+        }                                                                                                          \
+    } while (0)
+
+struct Layout {
+    uint64_t px;      // slab pixels (rows * width)
+    uint64_t nblk;    // 256-pixel blocks
+    uint64_t mask_at; // byte offset of the mask words
+    uint64_t bytes;   // header size
+};
+
+__host__ __device__ inline Layout layout(uint32_t width, uint32_t rows) {
+    Layout l;
+    l.px = (uint64_t)width * rows;
+    l.nblk = (l.px + SLAB_BLOCK - 1) / SLAB_BLOCK;
+    l.mask_at = (HDR_OFFS + l.nblk * 4 + 255) / 256 * 256;
+    l.bytes = l.mask_at + l.nblk * (SLAB_BLOCK / 8);
+    return l;
+}
+
+// global image row of slab row `lr` of `shard` (rt_launch's interleave), >= H past the image
+__host__ __device__ inline uint64_t global_row(uint64_t lr, uint32_t rb, uint32_t shard, uint32_t ns) {
+    return ((lr / rb) * ns + shard) * rb + lr % rb;
+}
+
+template <typename T>
+__device__ inline bool nonzero(const T *__restrict__ slab, uint64_t p) {
+    return (slab[p * 3] | slab[p * 3 + 1] | slab[p * 3 + 2]) != 0;
+}
+
+// one thread per slab pixel: mask words (one per wave) and the block's non-zero count
+template <typename T>
+__global__ __launch_bounds__(SLAB_BLOCK) void k_mask(const T *__restrict__ slab, uint32_t W, uint32_t H, uint32_t rb,
+                                                     uint32_t shard, uint32_t ns, uint64_t px,
+                                                     uint32_t *__restrict__ blk_cnt, uint64_t *__restrict__ mask) {
+    __shared__ uint32_t s_cnt[SLAB_BLOCK / 64];
+    const uint64_t p = (uint64_t)blockIdx.x * SLAB_BLOCK + threadIdx.x;
+    bool nz = false;
+    if (p < px && global_row(p / W, rb, shard, ns) < H) nz = nonzero(slab, p);
+    const uint64_t m = __ballot(nz);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        mask[p / 64] = m;
+        s_cnt[wave] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) blk_cnt[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+}
+
+// exclusive scan of the block counts in place (one workgroup, any count); the total to *count
+__global__ __launch_bounds__(1024) void k_scan(uint32_t *__restrict__ blk, uint64_t n, uint64_t *__restrict__ count) {
+    __shared__ uint64_t s_sum[1024];
+    const uint64_t t = threadIdx.x, per = (n + 1023) / 1024;
+    const uint64_t lo = t * per, hi = lo + per < n ? lo + per : n;
+    uint64_t acc = 0;
+    for (uint64_t i = lo; i < hi; ++i) acc += blk[i];
+    s_sum[t] = acc;
+    __syncthreads();
+    // Hillis-Steele over the 1024 partial sums
+    for (int off = 1; off < 1024; off <<= 1) {
+        const uint64_t u = t >= (uint64_t)off ? s_sum[t - off] : 0;
+        __syncthreads();
+        s_sum[t] += u;
+        __syncthreads();
+    }
+    uint64_t run = s_sum[t] - acc;
+    if (t == 1023) *count = s_sum[1023];
+    for (uint64_t i = lo; i < hi; ++i) {
+        const uint32_t x = blk[i];
+        blk[i] = (uint32_t)run; // < 2^32: the host checks px < 2^32
+        run += x;
+    }
+}
+
+// rank of slab pixel p among the non-zero pixels (its mask bit is set)
+__device__ inline uint64_t rank_of(const uint32_t *__restrict__ off, const uint64_t *__restrict__ mask, uint64_t p) {
+    const uint64_t w = p / 64, w0 = (p / SLAB_BLOCK) * (SLAB_BLOCK / 64);
+    uint64_t r = off[p / SLAB_BLOCK];
+    for (uint64_t i = w0; i < w; ++i) r += __popcll(mask[i]);
+    const uint64_t below = (1ull << (p % 64)) - 1ull;
+    return r + __popcll(mask[w] & below);
+}
+
+// non-zero pixels to their rank: the wave's mask word gives each lane its place
+template <typename T>
+__global__ __launch_bounds__(SLAB_BLOCK) void k_compact(const T *__restrict__ slab, uint64_t px,
+                                                        const uint32_t *__restrict__ off,
+                                                        const uint64_t *__restrict__ mask, T *__restrict__ vals) {
+    const uint64_t p = (uint64_t)blockIdx.x * SLAB_BLOCK + threadIdx.x;
+    if (p >= px) return;
+    if (!((mask[p / 64] >> (p % 64)) & 1ull)) return;
+    const uint64_t r = rank_of(off, mask, p);
+    vals[r * 3] = slab[p * 3];
+    vals[r * 3 + 1] = slab[p * 3 + 1];
+    vals[r * 3 + 2] = slab[p * 3 + 2];
+}
+
+struct ShardPtrs {
+    const unsigned char *hdr[RT_MAX_SHARDS];
+    const void *vals[RT_MAX_SHARDS];
+};
+
+// one thread per image pixel (x, g): shard and slab pixel from the interleave, then its value
+template <typename T>
+__global__ __launch_bounds__(SLAB_BLOCK) void k_unpack(ShardPtrs sp, uint64_t mask_at, uint32_t W, uint32_t H,
+                                                       uint32_t rb, uint32_t ns, T *__restrict__ image) {
+    const uint64_t i = (uint64_t)blockIdx.x * SLAB_BLOCK + threadIdx.x;
+    if (i >= (uint64_t)W * H) return;
+    const uint64_t g = i / W, x = i % W;
+    const uint32_t s = (uint32_t)((g / rb) % ns);
+    const uint64_t lr = (g / rb / ns) * rb + g % rb;
+    const uint64_t p = lr * W + x;
+    const unsigned char *h = sp.hdr[s];
+    const uint32_t *off = reinterpret_cast<const uint32_t *>(h + HDR_OFFS);
+    const uint64_t *mask = reinterpret_cast<const uint64_t *>(h + mask_at);
+    T c0 = 0, c1 = 0, c2 = 0;
+    if ((mask[p / 64] >> (p % 64)) & 1ull) {
+        const T *v = static_cast<const T *>(sp.vals[s]) + rank_of(off, mask, p) * 3;
+        c0 = v[0];
+        c1 = v[1];
+        c2 = v[2];
+    }
+    image[i * 3] = c0;
+    image[i * 3 + 1] = c1;
+    image[i * 3 + 2] = c2;
+}
+
+bool args_ok(uint32_t width, uint32_t height, uint32_t row_block, uint32_t nshards, int precision) {
+    if (width == 0 || height == 0 || row_block == 0 || nshards == 0 || nshards > RT_MAX_SHARDS) return false;
+    if (precision != RT_OUT_F64 && precision != RT_OUT_F32) return false;
+    return true;
+}
+
+} // namespace
+
+extern "C" {
+
+size_t rt_slab_header_bytes(uint32_t width, uint32_t height, uint32_t row_block, uint32_t nshards) {
+    if (width == 0 || row_block == 0 || nshards == 0) return 0;
+    return (size_t)layout(width, rt_shard_rows(height, row_block, nshards)).bytes;
+}
+
+int rt_slab_pack(const void *d_slab, uint32_t width, uint32_t height, uint32_t row_block, uint32_t shard,
+                 uint32_t nshards, int precision, void *d_header, void *d_values, void *stream) {
+    if (!d_slab || !d_header || !d_values || !args_ok(width, height, row_block, nshards, precision) ||
+        shard >= nshards)
+        return RT_EBADARG;
+    const Layout l = layout(width, rt_shard_rows(height, row_block, nshards));
+    if (l.px >= (1ull << 32)) return RT_ETOOBIG;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    unsigned char *h = static_cast<unsigned char *>(d_header);
+    uint64_t *count = reinterpret_cast<uint64_t *>(h);
+    uint32_t *off = reinterpret_cast<uint32_t *>(h + HDR_OFFS);
+    uint64_t *mask = reinterpret_cast<uint64_t *>(h + l.mask_at);
+    const dim3 grid((unsigned)l.nblk), blk(SLAB_BLOCK);
+    if (precision == RT_OUT_F32) {
+        hipLaunchKernelGGL(k_mask<uint32_t>, grid, blk, 0, st, static_cast<const uint32_t *>(d_slab), width, height,
+                           row_block, shard, nshards, l.px, off, mask);
+    } else {
+        hipLaunchKernelGGL(k_mask<uint64_t>, grid, blk, 0, st, static_cast<const uint64_t *>(d_slab), width, height,
+                           row_block, shard, nshards, l.px, off, mask);
+    }
+    SLABCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, off, l.nblk, count);
+    SLABCHK(hipGetLastError());
+    if (precision == RT_OUT_F32)
+        hipLaunchKernelGGL(k_compact<uint32_t>, grid, blk, 0, st, static_cast<const uint32_t *>(d_slab), l.px, off,
+                           mask, static_cast<uint32_t *>(d_values));
+    else
+        hipLaunchKernelGGL(k_compact<uint64_t>, grid, blk, 0, st, static_cast<const uint64_t *>(d_slab), l.px, off,
+                           mask, static_cast<uint64_t *>(d_values));
+    SLABCHK(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_slab_unpack(const void *const *d_headers, const void *const *d_values, uint32_t width, uint32_t height,
+                   uint32_t row_block, uint32_t nshards, int precision, void *d_image, void *stream) {
+    if (!d_headers || !d_values || !d_image || !args_ok(width, height, row_block, nshards, precision))
+        return RT_EBADARG;
+    const Layout l = layout(width, rt_shard_rows(height, row_block, nshards));
+    if (l.px >= (1ull << 32)) return RT_ETOOBIG;
+    ShardPtrs sp = {};
+    for (uint32_t s = 0; s < nshards; ++s) {
+        if (!d_headers[s] || !d_values[s]) return RT_EBADARG;
+        sp.hdr[s] = static_cast<const unsigned char *>(d_headers[s]);
+        sp.vals[s] = d_values[s];
+    }
+    const uint64_t n = (uint64_t)width * height;
+    const dim3 grid((unsigned)((n + SLAB_BLOCK - 1) / SLAB_BLOCK));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (precision == RT_OUT_F32)
+        hipLaunchKernelGGL(k_unpack<uint32_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, width, height, row_block,
+                           nshards, static_cast<uint32_t *>(d_image));
+    else
+        hipLaunchKernelGGL(k_unpack<uint64_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, width, height, row_block,
+                           nshards, static_cast<uint64_t *>(d_image));
+    SLABCHK(hipGetLastError());
+    return RT_OK;
+}
+
+} // extern "C"

@@ -113,6 +113,169 @@ class SlabPipeline:
         return out
 
 
+class SlabCodec:
+    """The HIP slab codec of the compact gather (rt_slab_pack / rt_slab_unpack,
+    include/rt_mi355x.h "compact slab transfer"): a slab becomes a fixed-size header (count,
+    per-256-pixel offsets, one bit per pixel) plus the non-background pixels' values; rank 0
+    decodes every shard straight into the row-major frame (rt_unshard fused with the decode).
+    Device tensors only: there is no host implementation in the product."""
+
+    def __init__(self, width: int, height: int, row_block: int, world: int, precision: str):
+        self.L = N.lib()
+        self.w, self.h, self.rb, self.world = width, height, row_block, world
+        self.prec = PRECISIONS[precision]
+        self.header_bytes = int(self.L.rt_slab_header_bytes(width, height, row_block, world))
+        if self.header_bytes == 0:
+            raise ValueError("rt_slab_header_bytes: bad frame arguments")
+
+    @staticmethod
+    def _stream(t):
+        import torch
+        return torch.cuda.current_stream(t.device).cuda_stream
+
+    def pack(self, slab, shard, header, values):
+        N.check(self.L.rt_slab_pack(slab.data_ptr(), self.w, self.h, self.rb, shard, self.world, self.prec,
+                                    header.data_ptr(), values.data_ptr(), self._stream(slab)), "rt_slab_pack")
+
+    def unpack(self, headers, values, frame):
+        n = len(headers)
+        hp = (ctypes.c_void_p * n)(*[h.data_ptr() for h in headers])
+        vp = (ctypes.c_void_p * n)(*[v.data_ptr() for v in values])
+        N.check(self.L.rt_slab_unpack(hp, vp, self.w, self.h, self.rb, n, self.prec, frame.data_ptr(),
+                                      self._stream(frame)), "rt_slab_unpack")
+
+
+class CompactGather:
+    """Pipelined compact gather of per-rank slabs to rank 0 (the default for world > 1).
+
+    Per frame i, on every rank: ``codec.pack`` encodes the slab just rendered (same stream);
+    the fixed-size headers are gathered to rank 0 (one collective), which also tells rank 0
+    every shard's value count; then each rank sends exactly its non-background values to
+    rank 0 (grouped point-to-point, RCCL over xGMI), and rank 0 decodes all shards into the
+    frame.  The exchange runs on a side stream, one frame behind the render: ``submit(i)``
+    issues frame i's header gather, frame i-1's value transfer (after reading its counts on
+    the host — by then frame i is already queued on the GPU) and frame i-2's decode, which it
+    returns on rank 0 (complete once ``frame_ready`` has fired: the decode runs on the side
+    stream, beside the next render).  ``drain()`` finishes the frames in flight.
+
+    Buffers form a ring of three frames; stream order makes reuse safe: frame i's pack runs
+    on the compute stream after frame i-3's decode and after the compute stream has waited for
+    frame i-3's transfer; every collective is issued on the side stream behind an event of
+    the pack it reads, so it never waits for a later render.
+    """
+
+    RING = 3
+
+    def __init__(self, codec, world, rank, slab_elems, dtype, device, frame, group=None):
+        import torch
+        self.torch = torch
+        self.codec, self.world, self.rank, self.group = codec, world, rank, group
+        self.frame = frame
+        self.cuda = torch.device(device).type == "cuda"
+        hb = codec.header_bytes
+        mk = lambda *shape, dt: torch.empty(shape, dtype=dt, device=device)  # noqa: E731
+        self.hdr = [mk(hb, dt=torch.uint8) for _ in range(self.RING)]
+        self.vals = [mk(slab_elems, dt=dtype) for _ in range(self.RING)]
+        self.ghdr = self.gvals = None
+        if rank == 0:
+            self.ghdr = [mk(world, hb, dt=torch.uint8) for _ in range(self.RING)]
+            self.gvals = [mk(world, slab_elems, dt=dtype) for _ in range(self.RING)]
+        self.xs = torch.cuda.Stream(device) if self.cuda else None
+        self.counts = torch.zeros(world, dtype=torch.int64, pin_memory=self.cuda)
+        self.i = 0
+        self.unpacked = [None] * self.RING  # rank 0: event after the decode of each slot
+        self.frame_ready = None             # rank 0: the last returned frame is complete after this
+        self.headed = []   # (ring slot, header gather work)
+        self.moving = []   # (ring slot, value transfer works)
+
+    def _side(self):
+        import contextlib
+        return self.torch.cuda.stream(self.xs) if self.cuda else contextlib.nullcontext()
+
+    def submit(self, slab, shard):
+        torch = self.torch
+        b = self.i % self.RING
+        self.i += 1
+        if self.unpacked[b] is not None:  # rank 0: slot b's last decode read vals[b]
+            torch.cuda.current_stream().wait_event(self.unpacked[b])
+            self.unpacked[b] = None
+        self.codec.pack(slab, shard, self.hdr[b], self.vals[b])
+        ev = None
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        out = None
+        if self.headed:
+            self._send(*self.headed.pop(0))
+        if len(self.moving) > 1:
+            out = self._finish(*self.moving.pop(0))
+        self._gather_headers(b, ev)
+        return out
+
+    def drain(self, on_frame=None):
+        """Finish every frame in flight (oldest first); ``on_frame(frame)`` sees each decoded
+        frame on rank 0 before the next one overwrites it.  Returns the last."""
+        out = None
+        while self.headed or self.moving:
+            if self.headed:
+                self._send(*self.headed.pop(0))
+            out = self._finish(*self.moving.pop(0))
+            if out is not None and on_frame is not None:
+                on_frame(out)
+        return out
+
+    def _gather_headers(self, b, ev):
+        import torch.distributed as dist
+        with self._side():
+            if ev is not None:
+                self.xs.wait_event(ev)
+            gl = list(self.ghdr[b].unbind(0)) if self.rank == 0 else None
+            w = dist.gather(self.hdr[b], gather_list=gl, dst=0, group=self.group, async_op=True)
+        self.headed.append((b, w))
+
+    def _send(self, b, work):
+        """Frame in slot b: its counts to the host, then the values to rank 0."""
+        torch = self.torch
+        import torch.distributed as dist
+        with self._side():
+            work.wait()
+            src = self.ghdr[b][:, :8] if self.rank == 0 else self.hdr[b][:8].unsqueeze(0)
+            cnt = src.contiguous().view(torch.int64).flatten()
+            self.counts[: cnt.numel()].copy_(cnt, non_blocking=self.cuda)
+            if self.cuda:
+                self.xs.synchronize()
+            counts = [int(c) for c in self.counts.tolist()]
+            # at least one pixel per message: every rank takes part in every batch
+            n = [max(c, 1) * 3 for c in counts]
+            ops = []
+            if self.rank == 0:
+                for s in range(1, self.world):
+                    ops.append(dist.P2POp(dist.irecv, self.gvals[b][s][: n[s]], s, group=self.group))
+            else:
+                ops.append(dist.P2POp(dist.isend, self.vals[b][: n[0]], 0, group=self.group))
+            works = dist.batch_isend_irecv(ops)
+        self.moving.append((b, works))
+
+    def _finish(self, b, works):
+        """Rank 0 decodes the frame in slot b on the side stream (beside the next render:
+        the decode is HBM-bound, the render FP64-bound); ``frame_ready`` marks its end.
+        Other ranks make the compute stream wait for their send before slot b is reused."""
+        if self.rank != 0:
+            for w in works:
+                w.wait()
+            return None
+        with self._side():
+            for w in works:
+                w.wait()
+            vals = [self.vals[b]] + [self.gvals[b][s] for s in range(1, self.world)]
+            self.codec.unpack(list(self.ghdr[b].unbind(0)), vals, self.frame)
+            if self.cuda:
+                self.frame_ready = self.torch.cuda.Event()
+                self.frame_ready.record()
+                self.unpacked[b] = self.frame_ready
+        return self.frame
+
+
 class FrameRenderer:
     """Renders this rank's rows of a W x H frame on its GPU and gathers the frame to rank 0.
 
@@ -130,6 +293,7 @@ class FrameRenderer:
         self.rank, self.world, self.rb, self.group = rank, world, row_block, group
         self.spp, self.seed = spp, seed
         self.prec, self.order = PRECISIONS[precision], ORDERS[order]
+        self.precision = precision
         self.dtype = torch.float64 if precision == "f64" else torch.float32
         self.device = torch.device("cuda", device)
         self.rows = shard_rows(height, row_block, world)
@@ -144,6 +308,7 @@ class FrameRenderer:
             self.gather_buf = torch.empty((world, self.rows, width, 3), dtype=self.dtype, device=self.device)
             self.frame = torch.empty((height, width, 3), dtype=self.dtype, device=self.device)
         self._pipe = None
+        self._cg = None
 
     def launch(self):
         st = self.torch.cuda.current_stream(self.device).cuda_stream
@@ -193,6 +358,24 @@ class FrameRenderer:
 
     def drain(self):
         return self._pipe.drain() if self._pipe is not None else None
+
+    # ---- compact gather (world > 1, the default in bench.py): background pixels not sent ----
+    def compact_gather(self):
+        if self._cg is None:
+            codec = SlabCodec(self.w, self.h, self.rb, self.world, self.precision)
+            self._cg = CompactGather(codec, self.world, self.rank, self.slab.numel(), self.dtype, self.device,
+                                     self.frame, self.group)
+        return self._cg
+
+    def step_compact(self):
+        """Render the next frame and hand it to the compact gather; returns (rank 0) the frame
+        two steps back once decoded, None otherwise.  drain_compact() finishes."""
+        cg = self.compact_gather()
+        self.launch()
+        return cg.submit(self.slab, self.rank)
+
+    def drain_compact(self):
+        return self._cg.drain() if self._cg is not None else None
 
     def close(self):
         if self._p:

@@ -180,6 +180,25 @@ int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dept
 int rt_unshard(const void *d_slabs, uint32_t width, uint32_t height, uint32_t row_block,
                uint32_t nshards, int precision, void *d_image, void *stream);
 int rt_release(rt_prepared *p);
+/* ---- compact slab transfer (the multi-GPU gather; raytracer.erl:151-161 collects pixels) --
+ * A slab (as rt_launch writes it) is mostly background pixels, +0.0 in all three channels.
+ * For the gather it is sent as a fixed-size header (count of non-zero pixels, u64 at byte
+ * 0; per 256 slab pixels the non-zero pixels before them; one bit per slab pixel) plus
+ * count*3 values of the slab's precision, the non-zero pixels in slab order.  The round trip
+ * is exact (bit patterns are copied; a pixel is zero iff its three channels are all-zero
+ * bits).  Slab rows past the image are not read and decode as zero.
+ * rt_slab_header_bytes: header size for one shard of this frame (0 for bad arguments).
+ * rt_slab_pack: encode shard `shard`'s slab on `stream`; d_values needs room for every slab
+ *   pixel (shard_rows*width*3 elements) in the worst case.
+ * rt_slab_unpack: decode nshards (<= RT_MAX_SHARDS) shards into the row-major image
+ *   ([H][W*3]) on `stream` — rt_unshard fused with the decode; d_headers[s] / d_values[s]
+ *   are device pointers to shard s's header and values. */
+#define RT_MAX_SHARDS 64
+size_t rt_slab_header_bytes(uint32_t width, uint32_t height, uint32_t row_block, uint32_t nshards);
+int rt_slab_pack(const void *d_slab, uint32_t width, uint32_t height, uint32_t row_block, uint32_t shard,
+                 uint32_t nshards, int precision, void *d_header, void *d_values, void *stream);
+int rt_slab_unpack(const void *const *d_headers, const void *const *d_values, uint32_t width, uint32_t height,
+                   uint32_t row_block, uint32_t nshards, int precision, void *d_image, void *stream);
 
 /* ---- P3 output: write_pixels_to_ppm/5 (raytracer.erl:667-685) -----------------------
  * The file is "P3\nW H\nMaxValue\n" followed, for every pixel in row order, by

@@ -111,3 +111,84 @@ def test_gloo_pipelined_gather_frames_in_order(tmp_path, world):
     for f in range(nframes):
         expect = (f * 1000.0 + np.arange(H, dtype=np.float64))[:, None] * np.ones((1, W))
         assert np.array_equal(frames[f], expect.astype(np.float32)), f"frame {f}"
+
+
+# ---- compact gather (dist.CompactGather, bench.py's default for world > 1) ----------------
+def _expected_frame(frame_no):
+    """Frame `frame_no`: pixel (x, r) holds a value when (x + r + frame_no) % 3 == 0, else the
+    background +0.0 — except pixel (1, 1), which holds (0, -0.0, 0): non-zero bits, so sent."""
+    g = torch.arange(H)
+    x = torch.arange(W)
+    val = (frame_no * 1000.0 + g[:, None] * 10.0 + x[None, :] / 64.0).float()
+    keep = (x[None, :] + g[:, None] + frame_no) % 3 == 0
+    z = torch.zeros(())
+    f = torch.stack([torch.where(keep, val, z), torch.where(keep, -val, z), torch.where(keep, val * 0.5, z)], -1)
+    if not keep[1, 1]:
+        f[1, 1, 1] = -0.0
+    return f
+
+
+def _sparse_slab(frame_no, rank, world, rows):
+    """`rank`'s slab of that frame; padding rows past the image hold garbage (never read)."""
+    g = torch.from_numpy(shard_global_rows(H, RB, world, rank))
+    slab = torch.full((rows, W, 3), 7.0)
+    ok = g >= 0
+    slab[ok] = _expected_frame(frame_no)[g[ok]]
+    return slab
+
+
+def _compact_worker(rank, world, port, out_path, nframes):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eraytracer_amd.dist import CompactGather
+    from tests.slab_ref import RefCodec
+    rows = shard_rows(H, RB, world)
+    codec = RefCodec(W, H, RB, world)
+    frame = torch.empty((H, W, 3), dtype=torch.float32) if rank == 0 else None
+    cg = CompactGather(codec, world, rank, rows * W * 3, torch.float32, "cpu", frame)
+    frames = []
+    for f in range(nframes):
+        out = cg.submit(_sparse_slab(f, rank, world, rows), rank)
+        if out is not None:
+            frames.append(out.clone())
+    cg.drain(on_frame=lambda fr: frames.append(fr.clone()))
+    if rank == 0:
+        np.save(out_path, torch.stack(frames).numpy())
+    else:
+        assert not frames
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_compact_gather_frames_in_order(tmp_path, world):
+    """CompactGather: headers gathered, exact value counts sent point-to-point, decoded on
+    rank 0, frames two deep in flight: every frame arrives complete, exact and in order."""
+    out = str(tmp_path / "frames.npy")
+    nframes = 6
+    mp.spawn(_compact_worker, args=(world, _free_port(), out, nframes), nprocs=world, join=True)
+    frames = np.load(out)
+    assert frames.shape == (nframes, H, W, 3)
+    for f in range(nframes):
+        assert np.array_equal(frames[f].view(np.int32), _expected_frame(f).numpy().view(np.int32)), f"frame {f}"
+
+
+def test_ref_codec_round_trip_and_layout():
+    from tests.slab_ref import RefCodec
+    for world in (1, 2, 3):
+        codec = RefCodec(W, H, RB, world)
+        rows = shard_rows(H, RB, world)
+        hdrs, vals = [], []
+        for s in range(world):
+            slab = _sparse_slab(2, s, world, rows)
+            h = torch.empty(codec.header_bytes, dtype=torch.uint8)
+            v = torch.full((rows * W * 3,), float("nan"))
+            codec.pack(slab, s, h, v)
+            n = int(h[:8].view(torch.int64)[0])
+            assert n == int(((slab.view(torch.int32) != 0).any(-1) & (torch.from_numpy(
+                shard_global_rows(H, RB, world, s)) >= 0)[:, None]).sum())
+            hdrs.append(h)
+            vals.append(v)
+        frame = torch.empty((H, W, 3))
+        codec.unpack(hdrs, vals, frame)
+        assert torch.equal(frame.view(torch.int32), _expected_frame(2).view(torch.int32))

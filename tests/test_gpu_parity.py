@@ -322,3 +322,93 @@ def test_launch_writes_only_image_rows(name, spp):
         assert not bool((buf[:h] == 12345.0).any())
     finally:
         L.rt_release(p)
+
+
+# ---- compact slab transfer (rt_slab_pack / rt_slab_unpack; dist.CompactGather) ----------
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+@pytest.mark.parametrize("w,h,rb,ns", [(80, 70, 16, 3), (64, 64, 16, 1), (33, 17, 4, 2), (100, 9, 16, 8),
+                                       (257, 31, 5, 4)])
+def test_slab_codec_matches_reference_format(prec, w, h, rb, ns):
+    """HIP pack gives the header and values of the test-side restatement byte for byte, on
+    random sparse slabs (-0.0 and NaN payloads count as non-zero; padding rows hold garbage);
+    HIP unpack reassembles the frame exactly."""
+    import torch
+
+    from eraytracer_amd.dist import SlabCodec, shard_global_rows
+    from tests.slab_ref import RefCodec
+    dt = torch.float32 if prec == "f32" else torch.float64
+    codec, ref = SlabCodec(w, h, rb, ns, prec), RefCodec(w, h, rb, ns)
+    assert codec.header_bytes == ref.header_bytes
+    rows = N.lib().rt_shard_rows(h, rb, ns)
+    gen = torch.Generator().manual_seed(w * 1000 + h * 10 + ns)
+    frame = torch.rand((h, w, 3), generator=gen, dtype=torch.float64).to(dt)
+    frame[torch.rand((h, w), generator=gen) < 0.7] = 0.0
+    frame[0, 0] = torch.tensor([0.0, -0.0, 0.0], dtype=dt)
+    frame[h - 1, w - 1, 2] = float("nan")
+    hdrs, vals = [], []
+    for s in range(ns):
+        g = shard_global_rows(h, rb, ns, s)
+        slab = torch.full((rows, w, 3), 5.0, dtype=dt)
+        slab[torch.from_numpy(g >= 0)] = frame[torch.from_numpy(g[g >= 0])]
+        hd = torch.full((codec.header_bytes,), 0xAB, dtype=torch.uint8, device="cuda")
+        vd = torch.full((rows * w * 3,), -9.0, dtype=dt, device="cuda")
+        codec.pack(slab.cuda(), s, hd, vd)
+        hr = torch.empty(ref.header_bytes, dtype=torch.uint8)
+        vr = torch.full((rows * w * 3,), -9.0, dtype=dt)
+        ref.pack(slab, s, hr, vr)
+        torch.cuda.synchronize()
+        n = int(hr[:8].view(torch.int64)[0])
+        hdc = hd.cpu()
+        # count, offsets and mask agree (bytes between the offsets and the mask are padding)
+        assert torch.equal(hdc[:8], hr[:8])
+        assert torch.equal(hdc[64:64 + 4 * ref.nblk], hr[64:64 + 4 * ref.nblk])
+        assert torch.equal(hdc[ref.mask_at:], hr[ref.mask_at:])
+        bits = torch.int32 if prec == "f32" else torch.int64
+        assert torch.equal(vd.cpu()[: 3 * n].view(bits), vr[: 3 * n].view(bits))
+        hdrs.append(hd)
+        vals.append(vd)
+    img = torch.full((h, w, 3), 3.0, dtype=dt, device="cuda")
+    codec.unpack(hdrs, vals, img)
+    torch.cuda.synchronize()
+    bits = torch.int32 if prec == "f32" else torch.int64
+    assert torch.equal(img.cpu().view(bits), frame.view(bits))
+
+
+def test_compact_gather_of_rendered_shards(oracle):
+    """rt_launch per shard -> rt_slab_pack -> rt_slab_unpack equals the single-shard frame bit
+    for bit (the multi-GPU compact gather's data path on one device)."""
+    import torch
+
+    from eraytracer_amd.dist import SlabCodec
+    L = N.lib()
+    scene = scenes.s64()
+    el = N.marshal(scene)
+    w, h, d, rb = 96, 75, 5, 16
+    p = ctypes.c_void_p()
+    N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(p)), "rt_prepare")
+    try:
+        st = torch.cuda.current_stream().cuda_stream
+        for prec, dt in ((N.RT_OUT_F32, torch.float32), (N.RT_OUT_F64, torch.float64)):
+            full = torch.empty((h, w, 3), dtype=dt, device="cuda")
+            N.check(L.rt_launch(p, w, h, d, rb, 0, 1, prec, N.RT_ORDER_EXACT, full.data_ptr(), None, st))
+            for ns in (2, 3, 8):
+                codec = SlabCodec(w, h, rb, ns, "f32" if prec == N.RT_OUT_F32 else "f64")
+                rows = L.rt_shard_rows(h, rb, ns)
+                hdrs, vals = [], []
+                for s in range(ns):
+                    slab = torch.full((rows, w, 3), float("nan"), dtype=dt, device="cuda")
+                    N.check(L.rt_launch(p, w, h, d, rb, s, ns, prec, N.RT_ORDER_EXACT, slab.data_ptr(), None, st))
+                    hdrs.append(torch.empty(codec.header_bytes, dtype=torch.uint8, device="cuda"))
+                    vals.append(torch.empty(rows * w * 3, dtype=dt, device="cuda"))
+                    codec.pack(slab, s, hdrs[-1], vals[-1])
+                img = torch.full_like(full, -1.0)
+                codec.unpack(hdrs, vals, img)
+                torch.cuda.synchronize()
+                assert torch.equal(img, full), f"nshards={ns}"
+                nz = int(sum(int(hd[:8].cpu().view(torch.int64)[0]) for hd in hdrs))
+                bits = torch.int32 if dt == torch.float32 else torch.int64
+                assert nz == int((full.view(bits) != 0).any(-1).sum())
+        ref, _ = _oracle(oracle, scene, w, h, d)
+        _check(full.cpu().numpy(), ref)
+    finally:
+        L.rt_release(p)
