@@ -28,6 +28,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Hardware queues per process (HIP's default, and the GPU box's setting, is 4): frames in
+# flight each use a stream of their own, and with RCCL's streams beside them 4 queues would be
+# shared behind event waits (measured: S64 4096^2 d5, 4 frames in flight, 0.68 ms per frame
+# with 4 queues, 0.61 with 8).  Set before the HIP runtime initialises.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 PEAK_FP64_VALU_TOPS = 39.3   # MI355X FP64 vector 78.6 TFLOP/s counting an FMA as 2 (spec); this path has no FMA
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
@@ -36,8 +42,8 @@ PEAK_HBM_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=50, help="untimed frames (the GPU's clocks settle over ~50)")
     ap.add_argument("--scene", default="s64")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--depth", type=int, default=5)
@@ -49,6 +55,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-boundary", action="store_true")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="frames in flight per rank (default 4 at N=1, 3 at N>1; 1 for --gather dense)")
     ap.add_argument("--gather", default="compact", choices=["compact", "dense"],
                     help="N > 1: compact = background pixels not sent (rt_slab_pack, default); dense = whole slabs")
     return ap.parse_args()
@@ -127,8 +135,9 @@ def main():
     W = H = args.size
     scene = scenes.named(args.scene)
     counts = workload.scene_counts(scene)
+    inflight = args.inflight or (1 if args.gather == "dense" and world > 1 else 4 if world == 1 else 3)
     fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
-                       precision=args.precision, order=args.order, spp=args.spp, seed=args.seed)
+                       precision=args.precision, order=args.order, spp=args.spp, seed=args.seed, inflight=inflight)
 
     # untimed: work count of this rank's rows (levels of every pixel's reflection chain)
     lv_fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
@@ -153,18 +162,15 @@ def main():
     if world > 1:
         pipe = fr.compact_gather() if args.gather == "compact" else fr.pipeline()
 
-    def one_step(e0=None, e1=None):
+    def one_step():
         if pipe is not None and args.gather == "dense":
             fr.slab = pipe.slab
-        if e0 is not None:
-            e0.record()
-        fr.launch()
-        if e1 is not None:
-            e1.record()
+        fr.launch()  # on the next in-flight slot's stream
         if pipe is None:
             fr.gather()
         elif args.gather == "compact":
-            pipe.submit(fr.slab, rank)
+            with torch.cuda.stream(fr.stream):
+                pipe.submit(fr.slab, rank)
         else:
             pipe.submit()
 
@@ -174,21 +180,26 @@ def main():
         pipe.drain()
     torch.cuda.synchronize()
 
-    # kernel-only timing of the render launches (events on the launch stream)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # GPU time of the timed region: HIP events on the caller's stream, every in-flight slot
+    # stream forked from it after the start event and joined into it before the end event
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    e0.record()
+    fr.fork()
     for i in range(args.steps):
-        one_step(*ev[i])
+        one_step()
     if pipe is not None:
         pipe.drain()
+    fr.join()
+    e1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = e0.elapsed_time(e1) / args.steps
 
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
@@ -231,7 +242,7 @@ def main():
             "config": {"workload": f"{args.scene.upper()} {W}x{H} depth {args.depth}"
                        + (f" x{args.spp} spp" if args.spp > 1 else ""), "scene": args.scene, "spp": args.spp,
                        "width": W, "height": H, "depth": args.depth, "order": args.order,
-                       "framebuffer": args.precision, "row_block": args.row_block,
+                       "framebuffer": args.precision, "row_block": args.row_block, "inflight": inflight,
                        "parallelism": f"rows{world}" + (f"+rccl_{args.gather}_gather" if world > 1 else ""),
                        "spheres": counts["spheres"], "triangles": counts["triangles"], "planes": counts["planes"],
                        "lights": counts["lights"]},
@@ -241,8 +252,8 @@ def main():
                          "executed_f64_frac": round(executed, 4) if executed is not None else None,
                          "note": "FP64 VALU (binding): algorithmic binary64 ops per frame launch as SURVEY.md 8d "
                                  f"counts them for the reference's brute-force scans ({ops_rank:.4g} ops for "
-                                 f"{px_rank} px) / mean launch time {kern_ms:.3f} ms (HIP events on the launch "
-                                 "stream); peak = 78.6 TFLOP/s FP64 vector / 2 (no FMA: contraction off). frac > 1 "
+                                 f"{px_rank} px) / GPU time per frame {kern_ms:.3f} ms (HIP events around the timed "
+                                 f"region, {inflight} frames in flight); peak = 78.6 TFLOP/s FP64 vector / 2 (no FMA: contraction off). frac > 1 "
                                  "means the beam/occluder culling skips reference work; executed_f64_frac is the "
                                  "FP64 instructions actually issued (rocprofv3 PMC, x64 lanes) / frame span / peak"
                                  + (f"; traffic and executed from {prof[1]}" if prof else "")},

@@ -26,11 +26,12 @@ RT_OUT_F64, RT_OUT_F32 = 0, 1
 RT_ORDER_EXACT, RT_ORDER_FAST = 0, 1
 RT_MAX_DEPTH = 16
 RT_MAX_SHARDS = 64
+RT_CFG_SIDE_STREAMS = 1
 
 # every symbol include/rt_mi355x.h declares (tests/test_boundary.py checks the export list)
 EXPORTS = (
     "rt_abi_version", "rt_strerror", "rt_device_count", "rt_scene_check", "rt_scene_canon",
-    "rt_render", "rt_prepare", "rt_shard_rows", "rt_launch", "rt_launch_spp", "rt_unshard", "rt_release",
+    "rt_render", "rt_prepare", "rt_shard_rows", "rt_launch", "rt_launch_spp", "rt_unshard", "rt_configure", "rt_release",
     "rt_ppm_bound", "rt_ppm_format", "rt_render_ppm_file",
     "rt_slab_header_bytes", "rt_slab_pack", "rt_slab_unpack",
 )
@@ -132,6 +133,7 @@ def lib() -> ctypes.CDLL:
     L.rt_render_ppm_file.argtypes = [vp, u32, u32, u32, u32, vp, u32, ctypes.c_char_p, vp]
     L.rt_unshard.argtypes = [vp, u32, u32, u32, u32, i32, vp, vp]
     L.rt_release.argtypes = [vp]
+    L.rt_configure.argtypes = [vp, i32, ctypes.c_int64]
     L.rt_slab_header_bytes.restype = ctypes.c_size_t
     L.rt_slab_header_bytes.argtypes = [u32, u32, u32, u32]
     L.rt_slab_pack.argtypes = [vp, u32, u32, u32, u32, u32, i32, vp, vp, vp]

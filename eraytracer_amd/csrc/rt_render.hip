@@ -969,6 +969,7 @@ struct rt_prepared {
     // sharing a queue block each other behind their event waits (measured: 5 streams, S64
     // 11 Gpx/s; 3 side streams were no faster than 2 — the chip is saturated in the overlap)
     hipStream_t side[2] = {};
+    int side_mode = -1; // rt_configure(RT_CFG_SIDE_STREAMS): -1 = environment (RT_LIT_STREAM), 0 off, 1 on
     hipEvent_t ev_level[RT_MAX_DEPTH + 1] = {}; // level k's list is ready
     hipEvent_t ev_lit[RT_MAX_DEPTH + 1] = {};   // level k is shaded
     // Frames repeat with identical arguments (bench, multi-GPU renderer): the second identical
@@ -1105,6 +1106,18 @@ int rt_prepare(const rt_elem *scene, uint32_t n, int device, rt_prepared **out) 
     return RT_OK;
 }
 
+int rt_configure(rt_prepared *p, int option, int64_t value) {
+    if (!p) return RT_EBADARG;
+    switch (option) {
+    case RT_CFG_SIDE_STREAMS:
+        if (value < -1 || value > 1) return RT_EBADARG;
+        p->side_mode = (int)value;
+        return RT_OK;
+    default:
+        return RT_EBADARG;
+    }
+}
+
 int rt_release(rt_prepared *p) {
     if (!p) return RT_EBADARG;
     DevGuard g(p->device);
@@ -1144,13 +1157,14 @@ size_t queue_budget() {
     return b;
 }
 
-// RT_LIT_STREAM=0 keeps the shading pass on the caller's stream (no overlap), for A/B runs.
-bool lit_overlap() {
-    static bool on = [] {
+// Shading beside the reflection chain on the context's two side streams: per context
+// (rt_configure RT_CFG_SIDE_STREAMS), else RT_LIT_STREAM=0 turns it off, for A/B runs.
+bool lit_overlap(const rt_prepared *p) {
+    static bool env_on = [] {
         const char *s = std::getenv("RT_LIT_STREAM");
         return !(s && std::strcmp(s, "0") == 0);
     }();
-    return on;
+    return p->side_mode < 0 ? env_on : p->side_mode != 0;
 }
 
 int side_stream(rt_prepared *p) {
@@ -1203,7 +1217,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     const size_t items_ints = slots * nlev + 64;
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_items), &p->items_bytes, items_ints * sizeof(int), &p->gen);
-    const bool overlap = lit_overlap() && D > 1 && p->hdr.n_light > 0;
+    const bool overlap = lit_overlap(p) && D > 1 && p->hdr.n_light > 0;
     if (rc == RT_OK && overlap) rc = side_stream(p);
     if (rc != RT_OK) return rc;
     // streams of the shading pass: level 0 (the bulk) beside the whole reflection chain, the

@@ -158,10 +158,10 @@ class CompactGather:
     returns on rank 0 (complete once ``frame_ready`` has fired: the decode runs on the side
     stream, beside the next render).  ``drain()`` finishes the frames in flight.
 
-    Buffers form a ring of three frames; stream order makes reuse safe: frame i's pack runs
-    on the compute stream after frame i-3's decode and after the compute stream has waited for
-    frame i-3's transfer; every collective is issued on the side stream behind an event of
-    the pack it reads, so it never waits for a later render.
+    Buffers form a ring of three frames.  Frame i's pack waits for the event that ends frame
+    i-3's send (rank 0: its decode), so the caller may render consecutive frames on different
+    streams; every collective is issued on the side stream behind an event of the pack it
+    reads, so it never waits for a later render.
     """
 
     RING = 3
@@ -183,7 +183,7 @@ class CompactGather:
         self.xs = torch.cuda.Stream(device) if self.cuda else None
         self.counts = torch.zeros(world, dtype=torch.int64, pin_memory=self.cuda)
         self.i = 0
-        self.unpacked = [None] * self.RING  # rank 0: event after the decode of each slot
+        self.free = [None] * self.RING      # event: the slot's last send (decode on rank 0) is done
         self.frame_ready = None             # rank 0: the last returned frame is complete after this
         self.headed = []   # (ring slot, header gather work)
         self.moving = []   # (ring slot, value transfer works)
@@ -196,9 +196,9 @@ class CompactGather:
         torch = self.torch
         b = self.i % self.RING
         self.i += 1
-        if self.unpacked[b] is not None:  # rank 0: slot b's last decode read vals[b]
-            torch.cuda.current_stream().wait_event(self.unpacked[b])
-            self.unpacked[b] = None
+        if self.free[b] is not None:  # slot b's last send / decode has read its buffers
+            torch.cuda.current_stream().wait_event(self.free[b])
+            self.free[b] = None
         self.codec.pack(slab, shard, self.hdr[b], self.vals[b])
         ev = None
         if self.cuda:
@@ -257,23 +257,23 @@ class CompactGather:
         self.moving.append((b, works))
 
     def _finish(self, b, works):
-        """Rank 0 decodes the frame in slot b on the side stream (beside the next render:
-        the decode is HBM-bound, the render FP64-bound); ``frame_ready`` marks its end.
-        Other ranks make the compute stream wait for their send before slot b is reused."""
-        if self.rank != 0:
-            for w in works:
-                w.wait()
-            return None
+        """Wait (on the side stream) for frame slot b's transfer; rank 0 then decodes it there,
+        beside the next render (the decode is HBM-bound, the render FP64-bound).  The event
+        ``free[b]`` marks slot b's buffers reusable; on rank 0 ``frame_ready`` marks the frame
+        complete."""
         with self._side():
             for w in works:
                 w.wait()
-            vals = [self.vals[b]] + [self.gvals[b][s] for s in range(1, self.world)]
-            self.codec.unpack(list(self.ghdr[b].unbind(0)), vals, self.frame)
+            if self.rank == 0:
+                vals = [self.vals[b]] + [self.gvals[b][s] for s in range(1, self.world)]
+                self.codec.unpack(list(self.ghdr[b].unbind(0)), vals, self.frame)
             if self.cuda:
-                self.frame_ready = self.torch.cuda.Event()
-                self.frame_ready.record()
-                self.unpacked[b] = self.frame_ready
-        return self.frame
+                ev = self.torch.cuda.Event()
+                ev.record()
+                self.free[b] = ev
+                if self.rank == 0:
+                    self.frame_ready = ev
+        return self.frame if self.rank == 0 else None
 
 
 class FrameRenderer:
@@ -281,11 +281,19 @@ class FrameRenderer:
 
     ``step()`` = one pass of the hot path over one frame: the render kernel on this
     rank's rows (rt_launch) and, for world > 1, the gather plus rank 0's reorder
-    (rt_unshard, two strided device copies)."""
+    (rt_unshard, two strided device copies).
+
+    ``inflight`` > 1 keeps that many frames in flight: one render context (rt_prepare:
+    its own work space), slab and HIP stream per slot, frames dealt to the slots in turn.  A
+    frame's reflection chain ends in a latency-bound tail (sparse deep levels, the chain
+    walk); the next frames' dense primary and shading kernels fill it.  Each context then
+    runs its kernels on its slot's stream alone (RT_CFG_SIDE_STREAMS = 0), so the process
+    stays within its hardware queues.  ``stream`` is the stream of the last launched frame;
+    work on that frame (the gather's pack) goes on it."""
 
     def __init__(self, scene, width: int, height: int, depth: int, *, rank: int = 0, world: int = 1,
                  device: int = 0, row_block: int = 16, precision: str = "f32", order: str = "exact", group=None,
-                 levels: bool = False, spp: int = 1, seed: int = 0):
+                 levels: bool = False, spp: int = 1, seed: int = 0, inflight: int = 1):
         import torch
         self.torch = torch
         self.L = N.lib()
@@ -297,10 +305,23 @@ class FrameRenderer:
         self.dtype = torch.float64 if precision == "f64" else torch.float32
         self.device = torch.device("cuda", device)
         self.rows = shard_rows(height, row_block, world)
+        if inflight < 1 or (inflight > 1 and levels):
+            raise ValueError("inflight must be >= 1 (and 1 with levels)")
         el = N.marshal(scene)
-        self._p = ctypes.c_void_p()
-        N.check(self.L.rt_prepare(el, len(el), device, ctypes.byref(self._p)), "rt_prepare")
-        self.slab = torch.empty((self.rows, width, 3), dtype=self.dtype, device=self.device)
+        self._ps = []
+        for _ in range(inflight):
+            p = ctypes.c_void_p()
+            N.check(self.L.rt_prepare(el, len(el), device, ctypes.byref(p)), "rt_prepare")
+            self._ps.append(p)
+            if inflight > 1:
+                N.check(self.L.rt_configure(p, N.RT_CFG_SIDE_STREAMS, 0), "rt_configure")
+        self._p = self._ps[0]
+        self.slabs = [torch.empty((self.rows, width, 3), dtype=self.dtype, device=self.device)
+                      for _ in range(inflight)]
+        self.slab = self.slabs[0]
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(inflight)] if inflight > 1 else None
+        self.stream = torch.cuda.current_stream(self.device)
+        self.n = 0
         self.levels = torch.empty((self.rows, width), dtype=torch.uint8, device=self.device) if levels else None
         self.gather_buf = None
         self.frame = None
@@ -311,10 +332,32 @@ class FrameRenderer:
         self._cg = None
 
     def launch(self):
-        st = self.torch.cuda.current_stream(self.device).cuda_stream
+        """Render the next frame: on the caller's current stream, or (inflight > 1) on the
+        next slot's stream into that slot's slab."""
+        j = self.n % len(self._ps)
+        self.n += 1
+        if self.streams is not None:
+            self.slab, self.stream = self.slabs[j], self.streams[j]
+        else:
+            self.stream = self.torch.cuda.current_stream(self.device)
         lv = self.levels.data_ptr() if self.levels is not None else None
-        N.check(self.L.rt_launch_spp(self._p, self.w, self.h, self.depth, self.rb, self.rank, self.world, self.prec,
-                                     self.order, self.spp, self.seed, self.slab.data_ptr(), lv, st), "rt_launch")
+        N.check(self.L.rt_launch_spp(self._ps[j], self.w, self.h, self.depth, self.rb, self.rank, self.world, self.prec,
+                                     self.order, self.spp, self.seed, self.slab.data_ptr(), lv,
+                                     self.stream.cuda_stream), "rt_launch")
+
+    def fork(self):
+        """Make every slot stream wait for the caller's current stream (start of a timed region)."""
+        if self.streams is not None:
+            cur = self.torch.cuda.current_stream(self.device)
+            for s in self.streams:
+                s.wait_stream(cur)
+
+    def join(self):
+        """Make the caller's current stream wait for every slot stream."""
+        if self.streams is not None:
+            cur = self.torch.cuda.current_stream(self.device)
+            for s in self.streams:
+                cur.wait_stream(s)
 
     def gather(self):
         if self.world == 1:
@@ -335,6 +378,8 @@ class FrameRenderer:
 
     # ---- pipelined frames (world > 1): render frame i+1 while frame i is gathered ----------
     def pipeline(self):
+        if self.streams is not None:
+            raise ValueError("the dense slab pipeline takes one frame in flight (inflight=1)")
         if self._pipe is None:
             torch = self.torch
             slabs = [self.slab, torch.empty_like(self.slab)]
@@ -372,15 +417,18 @@ class FrameRenderer:
         two steps back once decoded, None otherwise.  drain_compact() finishes."""
         cg = self.compact_gather()
         self.launch()
-        return cg.submit(self.slab, self.rank)
+        with self.torch.cuda.stream(self.stream):
+            return cg.submit(self.slab, self.rank)
 
     def drain_compact(self):
         return self._cg.drain() if self._cg is not None else None
 
     def close(self):
-        if self._p:
-            self.L.rt_release(self._p)
-            self._p = ctypes.c_void_p()
+        for p in self._ps:
+            if p:
+                self.L.rt_release(p)
+        self._ps = []
+        self._p = ctypes.c_void_p()
 
     def __del__(self):
         try:

@@ -180,6 +180,14 @@ int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dept
 int rt_unshard(const void *d_slabs, uint32_t width, uint32_t height, uint32_t row_block,
                uint32_t nshards, int precision, void *d_image, void *stream);
 int rt_release(rt_prepared *p);
+/* Per-context launch options.
+ * RT_CFG_SIDE_STREAMS: 1 = a frame's shading runs on two low-priority side streams of the
+ *   context beside its reflection chain (the fastest for ONE frame in flight); 0 = every
+ *   kernel on the caller's stream (for callers that keep several frames in flight on
+ *   their own streams, one context each: the frames then fill each other's latency-bound
+ *   tails); -1 = the default (on, unless the environment sets RT_LIT_STREAM=0). */
+#define RT_CFG_SIDE_STREAMS 1
+int rt_configure(rt_prepared *p, int option, int64_t value);
 /* ---- compact slab transfer (the multi-GPU gather; raytracer.erl:151-161 collects pixels) --
  * A slab (as rt_launch writes it) is mostly background pixels, +0.0 in all three channels.
  * For the gather it is sent as a fixed-size header (count of non-zero pixels, u64 at byte

@@ -412,3 +412,28 @@ def test_compact_gather_of_rendered_shards(oracle):
         _check(full.cpu().numpy(), ref)
     finally:
         L.rt_release(p)
+
+
+def test_frames_in_flight_match_single_frame():
+    """FrameRenderer(inflight=3) (bench.py's default mode): frames on three contexts and
+    streams at once, side streams off, each bit-identical to the one-context frame."""
+    import torch
+
+    from eraytracer_amd.dist import FrameRenderer
+    w, h, d = 128, 96, 5
+    one = FrameRenderer(scenes.s64(), w, h, d, precision="f64")
+    one.launch()
+    torch.cuda.synchronize()
+    ref = one.slab[:h].clone()
+    one.close()
+    fr = FrameRenderer(scenes.s64(), w, h, d, precision="f64", inflight=3)
+    outs = []
+    for _ in range(7):
+        fr.slab.fill_(float("nan")) if fr.n == 0 else None
+        fr.launch()
+        outs.append(fr.slab)
+    fr.join()
+    torch.cuda.synchronize()
+    for i, s in enumerate(fr.slabs):
+        assert torch.equal(s[:h], ref), f"slot {i}"
+    fr.close()
