@@ -427,11 +427,11 @@ def test_frames_in_flight_match_single_frame():
     ref = one.slab[:h].clone()
     one.close()
     fr = FrameRenderer(scenes.s64(), w, h, d, precision="f64", inflight=3)
-    outs = []
+    for s in fr.slabs:
+        s.fill_(float("nan"))
+    fr.fork()
     for _ in range(7):
-        fr.slab.fill_(float("nan")) if fr.n == 0 else None
         fr.launch()
-        outs.append(fr.slab)
     fr.join()
     torch.cuda.synchronize()
     for i, s in enumerate(fr.slabs):
