@@ -33,7 +33,7 @@ EXPORTS = (
     "rt_abi_version", "rt_strerror", "rt_device_count", "rt_scene_check", "rt_scene_canon",
     "rt_render", "rt_prepare", "rt_shard_rows", "rt_launch", "rt_launch_spp", "rt_unshard", "rt_configure", "rt_release",
     "rt_ppm_bound", "rt_ppm_format", "rt_render_ppm_file",
-    "rt_slab_header_bytes", "rt_slab_pack", "rt_slab_unpack",
+    "rt_slab_header_bytes", "rt_slab_pack", "rt_slab_unpack", "rt_selftest_math",
 )
 
 
@@ -134,6 +134,7 @@ def lib() -> ctypes.CDLL:
     L.rt_unshard.argtypes = [vp, u32, u32, u32, u32, i32, vp, vp]
     L.rt_release.argtypes = [vp]
     L.rt_configure.argtypes = [vp, i32, ctypes.c_int64]
+    L.rt_selftest_math.argtypes = [i32, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     L.rt_slab_header_bytes.restype = ctypes.c_size_t
     L.rt_slab_header_bytes.argtypes = [u32, u32, u32, u32]
     L.rt_slab_pack.argtypes = [vp, u32, u32, u32, u32, u32, i32, vp, vp, vp]

@@ -65,8 +65,55 @@ __device__ __forceinline__ double dot3(const D3 &a, const D3 &b) { // vector_dot
     return a.x * b.x + a.y * b.y + a.z * b.z;
 }
 
+// ---- correctly rounded sqrt and division, bit for bit the compiler's, minus range handling --
+// The device sqrt(double) is v_rsq_f64 refined by one Goldschmidt and two Newton steps, wrapped
+// in a scaling for inputs below 2^-767 and fix-ups for 0 and inf; 1.0/b is v_rcp_f64 refined
+// twice, one correction step, wrapped in v_div_scale / v_div_fmas / v_div_fixup, which leave
+// operands and results unchanged for normal-range values.  The *_n forms are those refinement
+// sequences alone (operand for operand, so the same bits) and are used only where every lane's
+// operand is inside the range where the wrappers are the identity; *_x check that for the wave
+// (one compare and a ballot) and otherwise take the full device sequence.  About 40 % fewer
+// VALU instructions per normalize, and the path is VALU-issue bound.
+constexpr double SQRT_N_LO = 0x1p-767, SQRT_N_HI = 0x1p1000;
+constexpr double RCP_N_LO = 0x1p-400, RCP_N_HI = 0x1p400;
+
+__device__ __forceinline__ double sqrt_n(double x) {
+    const double s = __builtin_amdgcn_rsq(x);
+    double g = x * s;
+    double h = s * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
+
+// a / b for |b| in [RCP_N_LO, RCP_N_HI] and |a| small enough that a/b is a normal number or 0
+__device__ __forceinline__ double div_n(double a, double b) {
+    double y = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-b, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    const double q = a * y;
+    const double r = __builtin_fma(-b, q, a);
+    return __builtin_fma(r, y, q);
+}
+
+__device__ __forceinline__ double sqrt_x(double x) { // == sqrt(x)
+    if (__ballot(!(x >= SQRT_N_LO && x <= SQRT_N_HI)) == 0) return sqrt_n(x);
+    return sqrt(x);
+}
+
 __device__ __forceinline__ D3 normalize3(const D3 &v) { // vector_normalize/1 (:554-560)
-    double mag = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+    const double m2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    if (__ballot(!(m2 >= RCP_N_LO && m2 <= RCP_N_HI)) == 0) { // mag and 1/mag in range, mag != 0
+        const double s = div_n(1.0, sqrt_n(m2));
+        return D3{v.x * s, v.y * s, v.z * s};
+    }
+    double mag = sqrt(m2);
     double s = 1.0 / mag;
     D3 r = {v.x * s, v.y * s, v.z * s};
     if (mag == 0) r = D3{0.0, 0.0, 0.0};
@@ -126,7 +173,7 @@ __device__ __forceinline__ double pow_libm(double x, double y) {
 __device__ __forceinline__ bool sph_t(double B, double C, double A4, double &t) {
     double disc = B * B - A4 * C;
     if (!(disc >= 0.001)) return false;
-    double sq = sqrt(disc);
+    double sq = sqrt_x(disc);
     double t0 = (-B + sq) / 2;
     double t1 = (-B - sq) / 2;
     if (!((t0 >= 0) && (t1 >= 0))) return false;
@@ -164,7 +211,7 @@ __device__ __forceinline__ bool sph_t_wave(double B, double C, double A4, double
     const bool ok = disc >= 0.001;
     t = 0.0;
     if (__ballot(ok) == 0) return false;
-    const double sq = sqrt(ok ? disc : 1.0);
+    const double sq = sqrt_x(ok ? disc : 1.0);
     const double t0 = (-B + sq) / 2;
     const double t1 = (-B - sq) / 2;
     t = (t1 < t0) ? t1 : t0;
@@ -391,7 +438,7 @@ __device__ __forceinline__ void scan_spheres(const Scene &S, int org, const D3 &
         const double disc0 = B0 * B0 - A4 * C0, disc1 = B1 * B1 - A4 * C1;
         const bool ok0 = disc0 >= 0.001, ok1 = disc1 >= 0.001;
         if (__ballot(ok0 | ok1) == 0) continue;
-        const double sq0 = sqrt(ok0 ? disc0 : 1.0), sq1 = sqrt(ok1 ? disc1 : 1.0);
+        const double sq0 = sqrt_x(ok0 ? disc0 : 1.0), sq1 = sqrt_x(ok1 ? disc1 : 1.0);
         const double a0 = (-B0 + sq0) / 2, b0 = (-B0 - sq0) / 2;
         const double a1 = (-B1 + sq1) / 2, b1 = (-B1 - sq1) / 2;
         const double t0 = (b0 < a0) ? b0 : a0, t1 = (b1 < a1) ? b1 : a1;
@@ -838,7 +885,7 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
     RT_STAT(ST_WAVES, 1);
 
     // primary ray: ray_through_pixel/3 (:510-511) at {X/Width, Y/Height} (:112)
-    const double X = (double)x / (double)W, Y = (double)gy / (double)H;
+    const double X = div_n((double)x, (double)W), Y = div_n((double)gy, (double)H); // == / (W, H <= 2^20)
     const double px = 0.0 + ((X - 0.5) * hdr.screen_w + hdr.sx);
     const double py = (Y - 0.5) * hdr.screen_h + hdr.sy;
     const D3 cam = {hdr.cam_x, hdr.cam_y, hdr.cam_z};
@@ -937,6 +984,36 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
 }
 
 #include "rt_wave.inc" // the wavefront engine (default)
+
+// rt_selftest_math: sqrt_n / div_n against the device library's sqrt and division, bit for bit,
+// on operands spread log-uniformly over the ranges where the kernels use them.
+__global__ __launch_bounds__(256) void k_selftest_math(unsigned long long n, unsigned long long seed,
+                                                       unsigned long long *__restrict__ bad) {
+    unsigned long long local = 0;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (unsigned long long)gridDim.x * 256) {
+        const unsigned long long r = splitmix64(seed ^ i), r2 = splitmix64(seed ^ ~i);
+        // sqrt over [2^-767, 2^1000]: random exponent, random 52-bit mantissa
+        const long long e = 1023 - 767 + (long long)((r >> 52) % (767 + 1000));
+        const double x = __longlong_as_double((long long)((unsigned long long)e << 52 | (r & 0xFFFFFFFFFFFFFull)));
+        if (__double_as_longlong(sqrt_n(x)) != __double_as_longlong(sqrt(x))) ++local;
+        // 1/b and a/b: b over [2^-400, 2^400], a an integer below 2^21 (the primary-ray divisions)
+        const long long eb = 1023 - 400 + (long long)((r2 >> 52) % 800);
+        const double b = __longlong_as_double((long long)((unsigned long long)eb << 52 | (r2 & 0xFFFFFFFFFFFFFull)));
+        if (__double_as_longlong(div_n(1.0, b)) != __double_as_longlong(1.0 / b)) ++local;
+        const double a = (double)(r >> 43), w = (double)((r2 >> 44) + 1);
+        if (__double_as_longlong(div_n(a, w)) != __double_as_longlong(a / w)) ++local;
+        // normalize3 on random vectors (both paths)
+        const D3 v = {x * (r & 1 ? 1 : -1) * 0x1p-600, b * 1e-3, a - 1e6};
+        const D3 u = normalize3(v);
+        const double m = sqrt(v.x * v.x + v.y * v.y + v.z * v.z), sc = 1.0 / m;
+        if (m != 0 && (__double_as_longlong(u.x) != __double_as_longlong(v.x * sc) ||
+                       __double_as_longlong(u.y) != __double_as_longlong(v.y * sc) ||
+                       __double_as_longlong(u.z) != __double_as_longlong(v.z * sc)))
+            ++local;
+    }
+    if (local) atomicAdd(bad, local);
+}
 
 } // namespace
 
@@ -1039,6 +1116,27 @@ int rt_debug_stats(unsigned long long *out, int n, int reset) {
 #endif
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_selftest_math(int device, uint64_t n, uint64_t seed, uint64_t *mismatches) {
+    if (!mismatches) return RT_EBADARG;
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return RT_ENODEV;
+    DevGuard g(device);
+    unsigned long long *d = nullptr;
+    if (hipMalloc(&d, sizeof(*d)) != hipSuccess) return RT_ENOMEM;
+    int rc = RT_OK;
+    if (hipMemset(d, 0, sizeof(*d)) != hipSuccess) rc = RT_EHIP;
+    if (rc == RT_OK) {
+        hipLaunchKernelGGL(k_selftest_math, dim3(4096), dim3(256), 0, nullptr, (unsigned long long)n,
+                           (unsigned long long)seed, d);
+        unsigned long long h = 0;
+        if (hipGetLastError() != hipSuccess || hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = RT_EHIP;
+        *mismatches = h;
+    }
+    (void)hipFree(d);
+    return rc;
+}
 
 const char *rt_strerror(int code) {
     switch (code) {

@@ -140,6 +140,12 @@ int rt_abi_version(void);
 const char *rt_strerror(int code);
 int rt_device_count(int *count);
 
+/* Diagnostic: the kernels' correctly rounded sqrt / division fast paths (rt_render.hip,
+ * sqrt_n / div_n: the device library's sequences without their range handling, used only
+ * where every operand of the wave is in range) against the library, bit for bit, on n random
+ * operands; *mismatches = the count of differing results (0 expected). */
+int rt_selftest_math(int device, uint64_t n, uint64_t seed, uint64_t *mismatches);
+
 /* Validate a scene list without rendering (0 = a scene the reference would
  * trace without crashing for a pixel that hits any object). */
 int rt_scene_check(const rt_elem *scene, uint32_t n_elems);
