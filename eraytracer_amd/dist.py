@@ -253,7 +253,7 @@ class CompactGather:
                     ops.append(dist.P2POp(dist.irecv, self.gvals[b][s][: n[s]], s, group=self.group))
             else:
                 ops.append(dist.P2POp(dist.isend, self.vals[b][: n[0]], 0, group=self.group))
-            works = dist.batch_isend_irecv(ops)
+            works = dist.batch_isend_irecv(ops) if ops else []  # a one-rank group sends nothing
         self.moving.append((b, works))
 
     def _finish(self, b, works):

@@ -445,3 +445,56 @@ def test_fast_sqrt_and_division_are_the_library_bits():
     bad = ctypes.c_uint64(123)
     N.check(N.lib().rt_selftest_math(0, 1 << 26, 0x5EED, ctypes.byref(bad)), "rt_selftest_math")
     assert bad.value == 0
+
+
+def test_compact_gather_pipeline_over_rccl_one_rank():
+    """dist.CompactGather end to end over RCCL (a one-rank nccl group: the GPU box has one
+    device) with three frames in flight on their own streams: the side stream, the events,
+    the pinned count read-back and the decode run as at N > 1, and every frame rank 0 gets
+    back equals the single-context frame bit for bit."""
+    import os
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from eraytracer_amd.dist import CompactGather, FrameRenderer, SlabCodec
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        w, h, d = 96, 80, 5
+        one = FrameRenderer(scenes.s64(), w, h, d, precision="f32")
+        one.launch()
+        torch.cuda.synchronize()
+        ref = one.slab[:h].clone()
+        one.close()
+        fr = FrameRenderer(scenes.s64(), w, h, d, precision="f32", inflight=3)
+        frame = torch.full((h, w, 3), float("nan"), dtype=torch.float32, device="cuda")
+        cg = CompactGather(SlabCodec(w, h, 16, 1, "f32"), 1, 0, fr.slab.numel(), torch.float32, fr.device, frame)
+        got = []
+
+        def keep(f):
+            torch.cuda.current_stream().wait_event(cg.frame_ready)
+            got.append(f.clone())
+            torch.cuda.synchronize()  # before the next decode overwrites the frame
+
+        fr.fork()
+        for _ in range(6):
+            fr.launch()
+            with torch.cuda.stream(fr.stream):
+                out = cg.submit(fr.slab, 0)
+            if out is not None:
+                keep(out)
+        cg.drain(on_frame=keep)
+        fr.join()
+        torch.cuda.synchronize()
+        assert len(got) == 6
+        for i, g in enumerate(got):
+            assert torch.equal(g, ref), f"frame {i}"
+        fr.close()
+    finally:
+        dist.destroy_process_group()

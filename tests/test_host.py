@@ -92,3 +92,37 @@ def test_work_model():
     c0 = dict(c, lights=0)
     assert workload.ops_from_levels([0, 1], 5, c0) == 31 + sc + 27 + 18
     assert np.array_equal(workload.levels_histogram(np.array([[0, 2], [2, 1]]), 3), [1, 1, 2, 0])
+
+
+def test_scene_compiler_under_host_sanitizers(tmp_path):
+    """The library's host code that parses caller input (rt_scene.cpp: check, canon, compile)
+    built with AddressSanitizer + UBSan (host only; GPU sanitizers are unavailable) and run on
+    the default, S64, S256 and adversarial scenes plus a truncated list and a lone camera."""
+    import shutil
+    import subprocess
+
+    from eraytracer_amd import _native as N
+    from tests.test_oracle import TRICKY
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "scene_check")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-ffp-contract=off", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", os.path.join(root, "tests", "csrc", "scene_check.cpp"),
+                    os.path.join(root, "eraytracer_amd", "csrc", "rt_scene.cpp"), "-o", exe], check=True)
+    scenes_ = [R.scene(), scenes.s64(), scenes.s256()] + [mk() for mk in TRICKY]
+    files = []
+    for i, sc in enumerate(scenes_):
+        el = N.marshal(sc)
+        p = tmp_path / f"s{i}.bin"
+        p.write_bytes(bytes(el))
+        files.append(str(p))
+    lone = tmp_path / "lone.bin"
+    lone.write_bytes(bytes(N.marshal(R.scene()[:1])))
+    files.append(str(lone))
+    r = subprocess.run([exe] + files, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rows = [ln.split() for ln in r.stdout.splitlines()]
+    assert len(rows) == len(files)
+    for row in rows[:len(scenes_)]:
+        assert row[0] == "0" and row[2] == "0", row  # valid scenes compile
