@@ -225,7 +225,18 @@ def main():
             f"-spp{args.spp}" if args.spp > 1 else "")
         prof = profile_for(wkey)
         traffic = prof[0]["hbm_bytes_per_launch"] if prof else None
-        executed = prof[0].get("derived", {}).get("f64_issue_frac_of_peak_39.3T") if prof else None
+        # executed work per frame from the profile's counters (counts do not depend on timing),
+        # over this run's live GPU time per frame: FP64 issue vs the FP64 peak, and VALU busy
+        # (a wave64 FP64 instruction holds a SIMD-32 for 4 cycles, other VALU ops for 2;
+        # 256 CUs x 4 SIMDs at 2.4 GHz)
+        executed = valu_busy = None
+        if prof:
+            c = prof[0].get("counters", {})
+            f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                              "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+            if f64 and c.get("SQ_INSTS_VALU"):
+                executed = f64 * 64 / k_s / (PEAK_FP64_VALU_TOPS * 1e12)
+                valu_busy = (4 * f64 + 2 * (c["SQ_INSTS_VALU"] - f64)) / (1024 * 2.4e9 * k_s)
         line = {
             "metric": "Mpixels/sec at 4096x4096, recursion depth 5 (frame rendered into HBM, gathered to rank 0)",
             "value": round(value, 3),
@@ -250,12 +261,15 @@ def main():
                          "unit": "TFLOP/s", "frac": round(valu_ach / PEAK_FP64_VALU_TOPS, 4),
                          "traffic": traffic,
                          "executed_f64_frac": round(executed, 4) if executed is not None else None,
+                         "valu_busy_frac": round(valu_busy, 4) if valu_busy is not None else None,
                          "note": "FP64 VALU (binding): algorithmic binary64 ops per frame launch as SURVEY.md 8d "
                                  f"counts them for the reference's brute-force scans ({ops_rank:.4g} ops for "
                                  f"{px_rank} px) / GPU time per frame {kern_ms:.3f} ms (HIP events around the timed "
                                  f"region, {inflight} frames in flight); peak = 78.6 TFLOP/s FP64 vector / 2 (no FMA: contraction off). frac > 1 "
-                                 "means the beam/occluder culling skips reference work; executed_f64_frac is the "
-                                 "FP64 instructions actually issued (rocprofv3 PMC, x64 lanes) / frame span / peak"
+                                 "means the beam/occluder culling skips reference work; executed_f64_frac = the FP64 "
+                                 "instructions actually issued per frame (rocprofv3 PMC, x64 lanes) / GPU time per "
+                                 "frame / peak; valu_busy_frac = SIMD cycles those VALU instructions occupy per frame "
+                                 "(FP64 4, others 2) / (1024 SIMDs x 2.4 GHz x GPU time per frame)"
                                  + (f"; traffic and executed from {prof[1]}" if prof else "")},
             "roofline_hbm": {"bound": "hbm", "achieved": round(hbm_ach, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": round(hbm_ach / PEAK_HBM_GBS, 6), "traffic": traffic},

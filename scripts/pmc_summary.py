@@ -2,7 +2,7 @@
 """Summarise a scripts/profile.sh run (rocprofv3 kernel trace + separate PMC passes) into one
 JSON (profiles/<name>.json) that DESIGN.md and bench.py cite.
 
-    python scripts/pmc_summary.py gpurun_out/TAG profiles/r01_TAG_pmc.json WORKLOAD_KEY
+    python scripts/pmc_summary.py gpurun_out/TAG profiles/r01_TAG_pmc.json WORKLOAD_KEY [TIMED_FRAMES]
 
 The unit is one FRAME LAUNCH (one rt_launch): the dispatch stream is cut into frames at each
 timed frame-start kernel (the wavefront engine's k_primary<PREC, false>, or the fused
@@ -82,7 +82,7 @@ def load_pmc(d):
     return frame, kern, dict(nfr)
 
 
-def load_trace(d):
+def load_trace(d, timed=None):
     f = glob.glob(os.path.join(d, "trace", "*kernel_trace.csv"))
     if not f:
         return None, None
@@ -103,8 +103,15 @@ def load_trace(d):
         for lab, (s, e, v) in f:
             per[lab].append(e - s)
             vg[lab] = v
+    # frames in flight overlap: the window from the first frame's first kernel to the last
+    # frame's last kernel, per frame, is the GPU time per frame the bench's events measure
+    # (over the last `timed` frames: the bench's timed region, after its warmup and a sync)
+    tf = fr[-timed:] if timed else fr
+    t_first = min(s for f in tf for _, (s, e, _) in f)
+    t_last = max(e for f in tf for _, (s, e, _) in f)
     frame = {"frames": len(fr), "kernels_per_frame": len(fr[0]), "avg_busy_ns": sum(busy) / len(busy),
-             "avg_span_ns": sum(span) / len(span), "min_busy_ns": min(busy)}
+             "avg_span_ns": sum(span) / len(span), "min_busy_ns": min(busy),
+             "window_ns_per_frame": (t_last - t_first) / len(tf), "window_frames": len(tf)}
     kern = {lab: {"avg_ns": sum(v) / len(v), "vgpr": vg[lab]} for lab, v in per.items()}
     return frame, kern
 
@@ -137,12 +144,13 @@ def derive(c, ns):
 
 def main():
     src, dst, key = sys.argv[1], sys.argv[2], sys.argv[3]
+    timed = int(sys.argv[4]) if len(sys.argv) > 4 else None  # the bench's --steps
     pmc, pmc_k, nfr = load_pmc(src)
-    tr, tr_k = load_trace(src)
+    tr, tr_k = load_trace(src, timed)
     out = {"workload": key, "source": os.path.basename(src.rstrip("/")), "unit": "one frame launch",
            "trace": tr, "counters": pmc, "frames_per_counter": nfr,
-           # frame-level rates over the frame's wall span (the engine's streams overlap)
-           "derived": derive(pmc, tr["avg_span_ns"] if tr else None), "kernels": {}}
+           # frame-level rates over the GPU time per frame (frames and streams overlap)
+           "derived": derive(pmc, tr["window_ns_per_frame"] if tr else None), "kernels": {}}
     for lab in sorted(set(pmc_k) | set(tr_k or {}), key=lambda s: (s.split("#")[0], int(s.split("#")[1]))):
         ent = dict((tr_k or {}).get(lab, {}))
         ent["counters"] = pmc_k.get(lab, {})
