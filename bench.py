@@ -45,7 +45,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50, help="untimed frames (the GPU's clocks settle over ~50)")
     ap.add_argument("--scene", default="s64")
-    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--size", type=int, default=4096, help="square frame side (see --width/--height)")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--order", default="exact", choices=["exact", "fast"])
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
@@ -132,7 +134,8 @@ def main():
         os.environ.setdefault("RT_LIT_STREAM", "0")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    W = H = args.size
+    W = args.width or args.size
+    H = args.height or args.size
     scene = scenes.named(args.scene)
     counts = workload.scene_counts(scene)
     inflight = args.inflight or (1 if args.gather == "dense" and world > 1 else 4 if world == 1 else 3)
