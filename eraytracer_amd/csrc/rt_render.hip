@@ -602,8 +602,10 @@ __device__ __forceinline__ void nearest_pair(const Scene &S, int org, const D3 &
     const double A40 = 4 * (d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
     const double A41 = 4 * (d1.x * d1.x + d1.y * d1.y + d1.z * d1.z);
     const Beam b = make_beam_pair(h, a0, d0, a1, d1);
+    RT_STAT(ST_NEAR_PRE, 1);
     for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
         unsigned long long m = b.on ? cull_chunk(S, b, chunk, org) : chunk_all(h.n_sph, chunk);
+        RT_STAT(ST_NEAR_PRE_CAND, __popcll(m));
         while (m) {
             const int k = chunk + __builtin_ctzll(m);
             m &= m - 1;
@@ -883,7 +885,14 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
     const int x = blockIdx.x * TILE + (wave & 1) * 8 + (lane & 7);
     const int ly = blockIdx.y * TILE + (wave >> 1) * 8 + (lane >> 3);
     const bool inside = x < W && ly < slab_rows;
-    const int gy = ((ly / rb) * nshards + shard) * rb + (ly % rb);
+    // slab row -> image row: the tile's first row split once (wave-uniform), the offset (< 16) added
+    const int ly_base = blockIdx.y * TILE, q_base = ly_base / rb;
+    int rr = ly_base - q_base * rb + (ly - ly_base), qq = q_base;
+    while (rr >= rb) {
+        rr -= rb;
+        ++qq;
+    }
+    const int gy = (qq * nshards + shard) * rb + rr;
     const bool active = inside && gy < H;
     RT_STAT(ST_WAVES, 1);
 

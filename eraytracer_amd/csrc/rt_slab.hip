@@ -3,7 +3,7 @@
 //
 // The reference's master collects every pixel from its workers (raytracer.erl:151-161,
 // :169-178); here each rank renders its interleaved rows into a slab in HBM and rank 0
-// gathers the slabs over xGMI.  Rendering runs at ~22 Gpx/s per MI355X, i.e. ~260 GB/s of
+// gathers the slabs over xGMI.  Rendering runs at ~27 Gpx/s per MI355X, i.e. ~325 GB/s of
 // f32 RGB per GPU, so with 8 ranks the gather into rank 0 (7 inbound links) and not the
 // render bounds a frame.  Most pixels are background (the reference's BACKGROUND_COLOUR,
 // raytracer.erl:186-203, exactly +0.0 in every channel: 73 % of S64's pixels), so a slab
@@ -18,8 +18,9 @@
 // Pack: k_mask (one wave per 64 pixels: ballot -> mask word, block popcount), k_scan (one
 // workgroup, exclusive scan of the block counts -> offsets and the count), k_compact
 // (non-zero pixels copied to their rank).  Unpack on rank 0 is fused with the reorder of
-// rt_unshard: one thread per image pixel finds its shard, slab pixel and mask bit and
-// reads its value, so the full frame is written once.
+// rt_unshard: one workgroup per image row and 256 columns (the row's shard and slab row are
+// wave-uniform), one thread per pixel finds its mask bit and reads its value, so the full
+// frame is written once.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -57,9 +58,15 @@ __host__ __device__ inline Layout layout(uint32_t width, uint32_t rows) {
     return l;
 }
 
-// global image row of slab row `lr` of `shard` (rt_launch's interleave), >= H past the image
-__host__ __device__ inline uint64_t global_row(uint64_t lr, uint32_t rb, uint32_t shard, uint32_t ns) {
-    return ((lr / rb) * ns + shard) * rb + lr % rb;
+// slab rows inside the image: a prefix of the slab (rt_launch's interleave)
+uint64_t valid_rows(uint32_t height, uint32_t rb, uint32_t shard, uint32_t ns, uint32_t rows) {
+    uint64_t n = 0;
+    for (uint64_t b = 0; b * rb < rows; ++b) {
+        const uint64_t g0 = (b * ns + shard) * rb;
+        if (g0 >= height) break;
+        n += (g0 + rb <= height) ? rb : height - g0;
+    }
+    return n;
 }
 
 template <typename T>
@@ -67,15 +74,15 @@ __device__ inline bool nonzero(const T *__restrict__ slab, uint64_t p) {
     return (slab[p * 3] | slab[p * 3 + 1] | slab[p * 3 + 2]) != 0;
 }
 
-// one thread per slab pixel: mask words (one per wave) and the block's non-zero count
+// one thread per slab pixel: mask words (one per wave) and the block's non-zero count.  The slab
+// rows inside the image are a prefix of the slab (global rows grow with slab rows), so a pixel
+// is in the image iff p < valid_px.
 template <typename T>
-__global__ __launch_bounds__(SLAB_BLOCK) void k_mask(const T *__restrict__ slab, uint32_t W, uint32_t H, uint32_t rb,
-                                                     uint32_t shard, uint32_t ns, uint64_t px,
+__global__ __launch_bounds__(SLAB_BLOCK) void k_mask(const T *__restrict__ slab, uint64_t valid_px,
                                                      uint32_t *__restrict__ blk_cnt, uint64_t *__restrict__ mask) {
     __shared__ uint32_t s_cnt[SLAB_BLOCK / 64];
     const uint64_t p = (uint64_t)blockIdx.x * SLAB_BLOCK + threadIdx.x;
-    bool nz = false;
-    if (p < px && global_row(p / W, rb, shard, ns) < H) nz = nonzero(slab, p);
+    const bool nz = p < valid_px && nonzero(slab, p);
     const uint64_t m = __ballot(nz);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) {
@@ -139,15 +146,16 @@ struct ShardPtrs {
     const void *vals[RT_MAX_SHARDS];
 };
 
-// one thread per image pixel (x, g): shard and slab pixel from the interleave, then its value
+// one workgroup per (image row g, 256 columns): the row's shard and slab row are wave-uniform
+// (no per-lane division), each lane finds its pixel's mask bit and value
 template <typename T>
-__global__ __launch_bounds__(SLAB_BLOCK) void k_unpack(ShardPtrs sp, uint64_t mask_at, uint32_t W, uint32_t H,
+__global__ __launch_bounds__(SLAB_BLOCK) void k_unpack(ShardPtrs sp, uint64_t mask_at, uint32_t W, uint32_t ncol,
                                                        uint32_t rb, uint32_t ns, T *__restrict__ image) {
-    const uint64_t i = (uint64_t)blockIdx.x * SLAB_BLOCK + threadIdx.x;
-    if (i >= (uint64_t)W * H) return;
-    const uint64_t g = i / W, x = i % W;
-    const uint32_t s = (uint32_t)((g / rb) % ns);
-    const uint64_t lr = (g / rb / ns) * rb + g % rb;
+    const uint32_t g = blockIdx.x / ncol, c = blockIdx.x - g * ncol;
+    const uint32_t x = c * SLAB_BLOCK + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t blk = g / rb, s = blk % ns;
+    const uint64_t lr = (uint64_t)(blk / ns) * rb + (g - blk * rb);
     const uint64_t p = lr * W + x;
     const unsigned char *h = sp.hdr[s];
     const uint32_t *off = reinterpret_cast<const uint32_t *>(h + HDR_OFFS);
@@ -159,9 +167,10 @@ __global__ __launch_bounds__(SLAB_BLOCK) void k_unpack(ShardPtrs sp, uint64_t ma
         c1 = v[1];
         c2 = v[2];
     }
-    image[i * 3] = c0;
-    image[i * 3 + 1] = c1;
-    image[i * 3 + 2] = c2;
+    T *o = image + ((uint64_t)g * W + x) * 3;
+    o[0] = c0;
+    o[1] = c1;
+    o[2] = c2;
 }
 
 bool args_ok(uint32_t width, uint32_t height, uint32_t row_block, uint32_t nshards, int precision) {
@@ -192,13 +201,14 @@ int rt_slab_pack(const void *d_slab, uint32_t width, uint32_t height, uint32_t r
     uint32_t *off = reinterpret_cast<uint32_t *>(h + HDR_OFFS);
     uint64_t *mask = reinterpret_cast<uint64_t *>(h + l.mask_at);
     const dim3 grid((unsigned)l.nblk), blk(SLAB_BLOCK);
-    if (precision == RT_OUT_F32) {
-        hipLaunchKernelGGL(k_mask<uint32_t>, grid, blk, 0, st, static_cast<const uint32_t *>(d_slab), width, height,
-                           row_block, shard, nshards, l.px, off, mask);
-    } else {
-        hipLaunchKernelGGL(k_mask<uint64_t>, grid, blk, 0, st, static_cast<const uint64_t *>(d_slab), width, height,
-                           row_block, shard, nshards, l.px, off, mask);
-    }
+    const uint64_t valid_px =
+        valid_rows(height, row_block, shard, nshards, rt_shard_rows(height, row_block, nshards)) * width;
+    if (precision == RT_OUT_F32)
+        hipLaunchKernelGGL(k_mask<uint32_t>, grid, blk, 0, st, static_cast<const uint32_t *>(d_slab), valid_px, off,
+                           mask);
+    else
+        hipLaunchKernelGGL(k_mask<uint64_t>, grid, blk, 0, st, static_cast<const uint64_t *>(d_slab), valid_px, off,
+                           mask);
     SLABCHK(hipGetLastError());
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, off, l.nblk, count);
     SLABCHK(hipGetLastError());
@@ -224,14 +234,16 @@ int rt_slab_unpack(const void *const *d_headers, const void *const *d_values, ui
         sp.hdr[s] = static_cast<const unsigned char *>(d_headers[s]);
         sp.vals[s] = d_values[s];
     }
-    const uint64_t n = (uint64_t)width * height;
-    const dim3 grid((unsigned)((n + SLAB_BLOCK - 1) / SLAB_BLOCK));
+    const uint32_t ncol = (width + SLAB_BLOCK - 1) / SLAB_BLOCK;
+    const uint64_t nblocks = (uint64_t)ncol * height;
+    if (nblocks >= (1ull << 31)) return RT_ETOOBIG;
+    const dim3 grid((unsigned)nblocks);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (precision == RT_OUT_F32)
-        hipLaunchKernelGGL(k_unpack<uint32_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, width, height, row_block,
+        hipLaunchKernelGGL(k_unpack<uint32_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, width, ncol, row_block,
                            nshards, static_cast<uint32_t *>(d_image));
     else
-        hipLaunchKernelGGL(k_unpack<uint64_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, width, height, row_block,
+        hipLaunchKernelGGL(k_unpack<uint64_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, width, ncol, row_block,
                            nshards, static_cast<uint64_t *>(d_image));
     SLABCHK(hipGetLastError());
     return RT_OK;
