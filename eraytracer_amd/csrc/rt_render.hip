@@ -1373,11 +1373,14 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                 HIPCHK(hipEventRecord(p->ev_level[k], st));
                 HIPCHK(hipStreamWaitEvent(ls(k), p->ev_level[k], 0));
             }
+            // levels >= 2 are shaded here only when dense (decided on the device; otherwise the
+            // launch exits at once): a smaller persistent grid keeps the empty launch cheap
+            const int lblocks = k >= 2 ? std::min(sblocks, DEEP_LIGHT_BLOCKS) : sblocks;
             if (sph_only)
-                hipLaunchKernelGGL((k_light<PREC, GENPOW, true>), dim3(sblocks), dim3(BLOCK), 0, ls(k), p->hdr,
+                hipLaunchKernelGGL((k_light<PREC, GENPOW, true>), dim3(lblocks), dim3(BLOCK), 0, ls(k), p->hdr,
                                    p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k));
             else
-                hipLaunchKernelGGL((k_light<PREC, GENPOW, false>), dim3(sblocks), dim3(BLOCK), 0, ls(k), p->hdr,
+                hipLaunchKernelGGL((k_light<PREC, GENPOW, false>), dim3(lblocks), dim3(BLOCK), 0, ls(k), p->hdr,
                                    p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k));
             HIPCHK(hipGetLastError());
             if (overlap) HIPCHK(hipEventRecord(p->ev_lit[k], ls(k)));
