@@ -1338,6 +1338,13 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     const int nshade = D > 0 ? 1 + nrefl : 0;
     // spheres only, culling on: every shadow target has occluder masks (lit_by<true>)
     const bool sph_only = p->hdr.n_tri == 0 && p->hdr.n_pl == 0 && p->hdr.cull_ok;
+    // no side streams (frames in flight): each level's shading fused into the next reflection
+    // pass (k_reflect_shade); RT_FUSE_SHADE=0 keeps separate k_light launches, for A/B runs
+    static const bool fuse_env = [] {
+        const char *e = std::getenv("RT_FUSE_SHADE");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    const bool fuse = fuse_env && !overlap && !levels && nrefl > 0;
     for (int row0 = 0; row0 < slab_rows; row0 += pass_rows) {
         const int rows = std::min(pass_rows, slab_rows - row0);
         const int ntiles = tiles_x * ((rows + TILE - 1) / TILE);
@@ -1373,6 +1380,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                 HIPCHK(hipEventRecord(p->ev_level[k], st));
                 HIPCHK(hipStreamWaitEvent(ls(k), p->ev_level[k], 0));
             }
+            if (fuse && k < nrefl) return RT_OK; // shaded by k_reflect_shade(k + 1)
             // levels >= 2 are shaded here only when dense (decided on the device; otherwise the
             // launch exits at once): a smaller persistent grid keeps the empty launch cheap
             const int lblocks = k >= 2 ? std::min(sblocks, DEEP_LIGHT_BLOCKS) : sblocks;
@@ -1390,7 +1398,17 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         for (int k = 1; k <= nrefl; ++k) {
             // level 1 (from the primary hits) is dense and throughput-bound; deeper levels are a few
             // waves each, bound by one wave's dependent chain: they walk two candidates per step
-            if (lv && k == 1)
+            if (fuse) {
+#define RT_RS(SPHV, ILPV)                                                                                           \
+    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, \
+                       p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1), colk(k - 1), \
+                       litk(k - 1))
+                if (sph_only && k == 1) RT_RS(true, false);
+                else if (sph_only) RT_RS(true, true);
+                else if (k == 1) RT_RS(false, false);
+                else RT_RS(false, true);
+#undef RT_RS
+            } else if (lv && k == 1)
                 hipLaunchKernelGGL((k_reflect<true, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
                                    p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1));
             else if (lv)

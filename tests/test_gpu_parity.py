@@ -498,3 +498,31 @@ def test_compact_gather_pipeline_over_rccl_one_rank():
         fr.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,w,h,d", [("default", 64, 48, 5), ("s64", 64, 64, 5), ("s256", 48, 40, 8),
+                                        ("default", 40, 30, 2)])
+def test_fused_reflect_shade_matches_oracle(oracle, name, w, h, d):
+    """Without side streams (frames in flight) each level's shading is fused into the next
+    reflection pass (k_reflect_shade): the frame equals the side-stream path's bit for bit
+    and the oracle within the bar, on spheres-only, mixed-object and dense-deep-level scenes."""
+    import torch
+    L = N.lib()
+    scene = scenes.named(name)
+    el = N.marshal(scene)
+    outs = []
+    for side in (1, 0):
+        p = ctypes.c_void_p()
+        N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(p)), "rt_prepare")
+        try:
+            N.check(L.rt_configure(p, N.RT_CFG_SIDE_STREAMS, side), "rt_configure")
+            img = torch.full((h, w, 3), float("nan"), dtype=torch.float64, device="cuda")
+            st = torch.cuda.current_stream().cuda_stream
+            N.check(L.rt_launch(p, w, h, d, 16, 0, 1, N.RT_OUT_F64, N.RT_ORDER_EXACT, img.data_ptr(), None, st))
+            torch.cuda.synchronize()
+            outs.append(img.cpu().numpy())
+        finally:
+            L.rt_release(p)
+    assert np.array_equal(outs[0].view(np.int64), outs[1].view(np.int64))
+    ref, _ = _oracle(oracle, scene, w, h, d)
+    _check(outs[1], ref)
