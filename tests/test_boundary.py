@@ -128,3 +128,18 @@ def test_render_without_device_fails_loudly(native):
         render(0, 6, R.scene(), 2)
     with pytest.raises(ValueError):
         render(8, 6, R.scene(), -1)
+
+
+def test_slab_header_size_and_configure_args(native):
+    """Host-only parts of the compact-gather codec and the per-context options: the header
+    size matches the documented layout (tests/slab_ref.py); bad arguments are refused."""
+    from tests.slab_ref import layout
+    L = native.lib()
+    for w, h, rb, ns in [(4096, 4096, 16, 8), (33, 17, 4, 2), (1, 1, 16, 1), (257, 31, 5, 4), (1920, 1080, 16, 3)]:
+        assert L.rt_slab_header_bytes(w, h, rb, ns) == layout(w, h, rb, ns)[3]
+    assert L.rt_slab_header_bytes(0, 10, 16, 1) == 0
+    assert L.rt_slab_header_bytes(10, 10, 0, 1) == 0
+    assert L.rt_configure(None, N.RT_CFG_SIDE_STREAMS, 0) == N.RT_EBADARG
+    assert L.rt_slab_pack(None, 8, 8, 16, 0, 1, N.RT_OUT_F32, None, None, None) == N.RT_EBADARG
+    bad = (ctypes.c_void_p * 1)(None)
+    assert L.rt_slab_unpack(bad, bad, 8, 8, 16, 1, N.RT_OUT_F32, None, None) == N.RT_EBADARG
