@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=1, help="samples per pixel (RT_SUPERSAMPLING; BASELINE config 5: 16)")
     ap.add_argument("--seed", type=int, default=0x5EED0005)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
+    ap.add_argument("--iso", type=int, default=20,
+                    help="frames launched back to back after the timed region to time the dominant kernel alone")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-boundary", action="store_true")
     ap.add_argument("--inflight", type=int, default=None,
@@ -74,7 +76,7 @@ def cpu_baseline(scene, W, H, depth, target_s, spp=1, seed=0):
     from oracle import oracle as O
     O.build()
     el = N.marshal(scene)
-    threads = min(16, os.cpu_count() or 1)
+    threads = O.host_threads()  # this process's CPU share (OMP_NUM_THREADS, else its CPU affinity)
     literal = spp == 1 and depth <= 5
     mode = O.LITERAL if literal else O.MEMO
     # calibrate on one row, then take evenly spaced rows to fill ~target_s seconds
@@ -93,7 +95,31 @@ def cpu_baseline(scene, W, H, depth, target_s, spp=1, seed=0):
     return {"value": px / dt / 1e6, "unit": "Mpixels/s", "cores": threads, "kind": "port",
             "sample": f"{len(rows)} evenly spaced rows x {W} px of the same {W}x{H} depth-{depth}"
                       + (f" x{spp} spp" if spp > 1 else "") + f" frame ({px} px, {dt:.1f} s), oracle/rt_oracle.c "
-                      f"{how}, {threads} threads; BEAM (erl) is not installed on the box"}
+                      f"{how}, {threads} threads; BEAM (erl) is not installed on the box",
+            "host": host_cpu_info()}
+
+
+def host_cpu_info():
+    """What the CPU baseline ran on: the machine's CPU count (nproc), the CPUs this process may
+    use (affinity), the cgroup CPU quota, OMP_NUM_THREADS and the CPU model."""
+    info = {"nproc": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity_cpus"] = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        info["cgroup_cpu_quota"] = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                info["cpu_model"] = ln.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return info
 
 
 def profile_for(workload_key):
@@ -111,12 +137,36 @@ def profile_for(workload_key):
     return best
 
 
+# The dominant kernel of each engine (the roofline's subject) and its label in the profiles
+# (scripts/pmc_summary.py: name#i = i-th launch of that kernel within a frame)
+DOMINANT = {"wave": ("k_reflect_shade#0", "RT_KT_LEVEL1",
+                     "k_reflect_shade(1): level-0 shading + level-1 reflection scan"),
+            "fused": ("k_render#0", "RT_KT_RENDER", "k_render: the fused engine's one kernel per frame")}
+
+
+def engine_of(counts, spp):
+    """The engine rt_launch picks (rt_render.hip use_mega_engine; RT_ENGINE forces one)."""
+    env = os.environ.get("RT_ENGINE")
+    if env in ("fused", "mega"):
+        return "fused"
+    if env == "wave" or spp > 1:
+        return "wave"
+    n_obj = counts["spheres"] + counts["triangles"] + counts["planes"]
+    return "fused" if n_obj <= int(os.environ.get("RT_FUSED_MAX_OBJECTS", "40")) else "wave"
+
+
+def f64_insts(c):
+    return sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                       "SQ_INSTS_VALU_TRANS_F64"))
+
+
 def main():
     args = parse()
     import numpy as np
     import torch
     import torch.distributed as dist
 
+    from eraytracer_amd import _native as N
     from eraytracer_amd import scenes, workload
     from eraytracer_amd.dist import FrameRenderer
 
@@ -162,8 +212,11 @@ def main():
     # The compact gather (default) sends only the non-background pixels: rank 0's inbound xGMI
     # links, not the render, bound a frame at N = 8 (dist.CompactGather).
     pipe = None
+    checked = None
     if world > 1:
         pipe = fr.compact_gather() if args.gather == "compact" else fr.pipeline()
+        if args.gather == "compact":
+            checked = self_check(fr, pipe, scene, args, rank, world, local)
 
     def one_step():
         if pipe is not None and args.gather == "dense":
@@ -184,7 +237,11 @@ def main():
     torch.cuda.synchronize()
 
     # GPU time of the timed region: HIP events on the caller's stream, every in-flight slot
-    # stream forked from it after the start event and joined into it before the end event
+    # stream forked from it after the start event and joined into it before the end event;
+    # the dominant kernel's launches are bracketed by events on their own streams
+    engine = engine_of(counts, args.spp)
+    dom_label, dom_kt, dom_desc = DOMINANT[engine]
+    fr.time_kernels(getattr(N, dom_kt))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
@@ -197,12 +254,21 @@ def main():
     if pipe is not None:
         pipe.drain()
     fr.join()
+    if pipe is not None and getattr(pipe, "xs", None) is not None:
+        torch.cuda.current_stream().wait_stream(pipe.xs)  # the last frames' exchange and decode
     e1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps
+    span_ms, span_n = fr.kernel_time(getattr(N, dom_kt))
+    fr.time_kernels(0)
+    # The dominant kernel alone: with frames in flight a launch's events also span the time it
+    # queues behind other frames' kernels, so its duration is timed again over args.iso frames
+    # launched back to back on one context and stream (consecutive launches serialise; rocprof's
+    # trace of the same run shows these as the last frames: scripts/pmc_summary.py "isolated")
+    dom_ms, dom_n = isolated_kernel_time(fr, getattr(N, dom_kt), args.iso) if args.iso > 0 else (None, 0)
 
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
@@ -220,26 +286,58 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         value = frame_px * args.steps / elapsed / 1e6
         bytes_px = 12 if args.precision == "f32" else 24
-        # roofline of the dominant kernel (this rank's render launch), per launch
         k_s = kern_ms / 1e3
-        valu_ach = ops_rank / k_s / 1e12
         hbm_ach = px_rank * bytes_px / k_s / 1e9
         wkey = f"{args.scene}-{W}x{H}-d{args.depth}-{args.order}-{args.precision}-n{world}" + (
             f"-spp{args.spp}" if args.spp > 1 else "")
         prof = profile_for(wkey)
-        traffic = prof[0]["hbm_bytes_per_launch"] if prof else None
-        # executed work per frame from the profile's counters (counts do not depend on timing),
-        # over this run's live GPU time per frame: FP64 issue vs the FP64 peak, and VALU busy
-        # (a wave64 FP64 instruction holds a SIMD-32 for 4 cycles, other VALU ops for 2;
-        # 256 CUs x 4 SIMDs at 2.4 GHz)
-        executed = valu_busy = None
+        # Roofline of the dominant kernel: its executed binary64 work per launch (the FP64
+        # wave-instructions the committed rocprofv3 PMC profile of this workload counts for it,
+        # x 64 lanes; counts do not depend on timing) over its average launch duration measured
+        # live in the timed region (HIP events on its own stream).  Peak: 39.3 T lane-ops/s
+        # (78.6 TFLOP/s FP64 vector counting an FMA as 2; a wave64 FP64 op issues over 4 cycles).
+        roof = {"bound": "valu", "kernel": dom_label.split("#")[0], "what": dom_desc, "peak": PEAK_FP64_VALU_TOPS,
+                "unit": "TFLOP/s", "achieved": None, "frac": None, "traffic": None,
+                "launch_ms_live": round(dom_ms, 4) if dom_ms else None, "launches_timed": dom_n,
+                "launch_span_ms_in_flight": round(span_ms, 4) if span_ms else None}
+        frame_exec = valu_busy = traffic_frame = None
         if prof:
-            c = prof[0].get("counters", {})
-            f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
-                                              "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
-            if f64 and c.get("SQ_INSTS_VALU"):
-                executed = f64 * 64 / k_s / (PEAK_FP64_VALU_TOPS * 1e12)
-                valu_busy = (4 * f64 + 2 * (c["SQ_INSTS_VALU"] - f64)) / (1024 * 2.4e9 * k_s)
+            d, path = prof
+            kd = d.get("kernels", {}).get(dom_label, {})
+            f64 = f64_insts(kd.get("counters", {}))
+            if f64 and dom_ms:
+                ach = f64 * 64 / (dom_ms / 1e3) / 1e12
+                roof.update(achieved=round(ach, 3), frac=round(ach / PEAK_FP64_VALU_TOPS, 4),
+                            f64_wave_insts_per_launch=round(f64))
+            kc = kd.get("counters", {})
+            if "FETCH_SIZE" in kc and "WRITE_SIZE" in kc:  # KiB; FETCH x2 on gfx950 (MI355X_MICROARCH.md)
+                roof["traffic"] = round((2 * kc["FETCH_SIZE"] + kc["WRITE_SIZE"]) * 1024)
+            if kd.get("isolated_avg_ns"):
+                roof["launch_ms_rocprof"] = round(kd["isolated_avg_ns"] / 1e6, 4)
+            if kd.get("avg_ns"):
+                roof["launch_ms_rocprof_in_flight"] = round(kd["avg_ns"] / 1e6, 4)
+            roof["profile"] = path
+            c = d.get("counters", {})
+            per = d.get("spp", 1)  # a supersampled profile's unit is one sample pass: spp per frame
+            f64f = f64_insts(c) * per
+            if f64f and c.get("SQ_INSTS_VALU"):
+                frame_exec = f64f * 64 / k_s / (PEAK_FP64_VALU_TOPS * 1e12)
+                valu_busy = (4 * f64f + 2 * (c["SQ_INSTS_VALU"] * per - f64f)) / (1024 * 2.4e9 * k_s)
+            if d.get("hbm_bytes_per_launch") is not None:
+                traffic_frame = d["hbm_bytes_per_launch"] * per
+        roof["frame_f64_issue_frac"] = round(frame_exec, 4) if frame_exec is not None else None
+        roof["frame_valu_busy_frac"] = round(valu_busy, 4) if valu_busy is not None else None
+        roof["ref_work_tops"] = round(ops_rank / k_s / 1e12, 3)
+        roof["note"] = ("FP64 VALU roofline (binding; MFMA does not apply, HBM does not bind): achieved = "
+                        "the dominant kernel's executed FP64 wave-instructions per launch (rocprofv3 PMC, "
+                        "profile named) x 64 lanes / its average launch duration measured live with HIP events "
+                        f"on its stream over {args.iso} frames launched back to back after the timed region (in "
+                        f"the timed region {inflight} frames in flight share the GPU and a launch's events also "
+                        "span its queueing: launch_span_ms_in_flight); launch_ms_rocprof = rocprofv3's average "
+                        "duration of the same launches; traffic = that kernel's HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE). frame_f64_issue_frac / frame_valu_busy_frac: "
+                        "all of a frame's kernels over the GPU time per frame. ref_work_tops: the reference's "
+                        "brute-force binary64 op count per frame (SURVEY.md 8d) / GPU time per frame, in T op/s "
+                        "(culling skips most of it: not a roofline)")
         line = {
             "metric": "Mpixels/sec at 4096x4096, recursion depth 5 (frame rendered into HBM, gathered to rank 0)",
             "value": round(value, 3),
@@ -257,58 +355,25 @@ def main():
                        + (f" x{args.spp} spp" if args.spp > 1 else ""), "scene": args.scene, "spp": args.spp,
                        "width": W, "height": H, "depth": args.depth, "order": args.order,
                        "framebuffer": args.precision, "row_block": args.row_block, "inflight": inflight,
+                       "engine": engine,
                        "parallelism": f"rows{world}" + (f"+rccl_{args.gather}_gather" if world > 1 else ""),
+                       "world_size": world, "rccl_ranks": dist.get_world_size() if world > 1 else 1,
                        "spheres": counts["spheres"], "triangles": counts["triangles"], "planes": counts["planes"],
                        "lights": counts["lights"]},
-            "roofline": {"bound": "valu", "achieved": round(valu_ach, 3), "peak": PEAK_FP64_VALU_TOPS,
-                         "unit": "TFLOP/s", "frac": round(valu_ach / PEAK_FP64_VALU_TOPS, 4),
-                         "traffic": traffic,
-                         "executed_f64_frac": round(executed, 4) if executed is not None else None,
-                         "valu_busy_frac": round(valu_busy, 4) if valu_busy is not None else None,
-                         "note": "FP64 VALU (binding): algorithmic binary64 ops per frame launch as SURVEY.md 8d "
-                                 f"counts them for the reference's brute-force scans ({ops_rank:.4g} ops for "
-                                 f"{px_rank} px) / GPU time per frame {kern_ms:.3f} ms (HIP events around the timed "
-                                 f"region, {inflight} frames in flight); peak = 78.6 TFLOP/s FP64 vector / 2 (no FMA: contraction off). frac > 1 "
-                                 "means the beam/occluder culling skips reference work; executed_f64_frac = the FP64 "
-                                 "instructions actually issued per frame (rocprofv3 PMC, x64 lanes) / GPU time per "
-                                 "frame / peak; valu_busy_frac = SIMD cycles those VALU instructions occupy per frame "
-                                 "(FP64 4, others 2) / (1024 SIMDs x 2.4 GHz x GPU time per frame)"
-                                 + (f"; traffic and executed from {prof[1]}" if prof else "")},
+            "roofline": roof,
             "roofline_hbm": {"bound": "hbm", "achieved": round(hbm_ach, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": round(hbm_ach / PEAK_HBM_GBS, 6), "traffic": traffic},
+                             "frac": round(hbm_ach / PEAK_HBM_GBS, 6), "traffic": traffic_frame,
+                             "note": "algorithmic bytes: the framebuffer store (12 B/px f32, 24 f64) per GPU time per "
+                                     "frame; traffic = measured HBM bytes per frame launch (PMC)"},
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_max_rank": round(kern_ms_max, 4),
             "kernel_mpx_s": round(px_rank / k_s / 1e6, 3),
             "ops_per_frame": ops_total,
         }
+        if checked is not None:
+            line["self_check"] = checked
         if world == 1 and not args.no_boundary:
-            from eraytracer_amd.raytracer import render
-            st = {}
-            render(W, H, scene, args.depth, precision=args.precision, order=args.order, stats=st, spp=args.spp,
-                   seed=args.seed)
-            ts = []
-            for _ in range(2):
-                st = {}
-                render(W, H, scene, args.depth, precision=args.precision, order=args.order, stats=st, spp=args.spp,
-                       seed=args.seed)
-                ts.append(st["total_ms"])
-            line["boundary_mpx_s"] = round(frame_px / (min(ts) / 1e3) / 1e6, 3)
-            # raytrace/5 end to end natively: render + P3 text on the GPU + file write
-            # (write_pixels_to_ppm/5, byte-exact); the binary64 frame never leaves the GPU
-            import tempfile
-            from eraytracer_amd.raytracer import render_ppm_file
-            with tempfile.TemporaryDirectory() as td:
-                path = os.path.join(td, "frame.ppm")
-                # one untimed call first: the first rt_render_ppm_file of a process pays ~2 s of
-                # one-time set-up (scripts/p3_timing.py), the other legs are timed warm too
-                render_ppm_file(W, H, scene, args.depth, path, spp=args.spp, seed=args.seed)
-                tp = []
-                for _ in range(3):
-                    t1 = time.perf_counter()
-                    render_ppm_file(W, H, scene, args.depth, path, spp=args.spp, seed=args.seed)
-                    tp.append(time.perf_counter() - t1)
-                line["p3_file_mpx_s"] = round(frame_px / min(tp) / 1e6, 3)
-                line["p3_file_bytes"] = os.path.getsize(path)
+            line.update(boundary_legs(N, scene, W, H, args))
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, W, H, args.depth, args.cpu_seconds, args.spp, args.seed)
         print(json.dumps(line), flush=True)
@@ -316,6 +381,93 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def isolated_kernel_time(fr, kernel, frames):
+    """Average duration of `kernel` (RT_KT_*) over `frames` frames launched back to back on the
+    first slot's context and stream (one frame in flight: each launch runs alone)."""
+    import torch
+    fr.time_kernels(kernel)
+    for _ in range(frames):
+        fr.launch_on(0)
+    torch.cuda.synchronize()
+    ms, n = fr.kernel_time(kernel)
+    fr.time_kernels(0)
+    return ms, n
+
+
+def self_check(fr, pipe, scene, args, rank, world, local):
+    """Before timing: a small check frame through this rank's render and the same compact gather
+    the timed loop uses; rank 0 compares each reassembled frame bit for bit with a one-shard
+    render of the frame (dist.verify_compact_gather).  The check frames share the frame size
+    (the gather's buffers are sized for it) but run the scene at depth 1 and 2."""
+    import ctypes
+
+    import torch
+
+    from eraytracer_amd import _native as N
+    from eraytracer_amd.dist import verify_compact_gather
+    L = N.lib()
+    depths = [1, 2]
+
+    def make_slab(i):
+        slab = fr.slabs[0]
+        N.check(L.rt_launch_spp(fr._ps[0], fr.w, fr.h, depths[i], fr.rb, rank, world, fr.prec, fr.order, fr.spp,
+                                fr.seed, slab.data_ptr(), None, torch.cuda.current_stream().cuda_stream))
+        return slab
+
+    def reference(i):
+        el = N.marshal(scene)
+        p = ctypes.c_void_p()
+        N.check(L.rt_prepare(el, len(el), local, ctypes.byref(p)))
+        try:
+            out = torch.empty((fr.h, fr.w, 3), dtype=fr.dtype, device=fr.device)
+            N.check(L.rt_launch_spp(p, fr.w, fr.h, depths[i], fr.rb, 0, 1, fr.prec, fr.order, fr.spp, fr.seed,
+                                    out.data_ptr(), None, torch.cuda.current_stream().cuda_stream))
+            torch.cuda.synchronize()
+            return out
+        finally:
+            L.rt_release(p)
+
+    n = verify_compact_gather(pipe, make_slab, reference, rank, nframes=len(depths))
+    torch.cuda.synchronize()
+    return {"frames": n, "equal_bitwise": True, "what": "compact-gathered frames == one-shard rt_launch frames"} \
+        if rank == 0 else None
+
+
+def boundary_legs(N, scene, W, H, args):
+    """The C-ABI boundary the BEAM NIF uses (rt_render: persistent context, row bands whose
+    copies overlap the next band's render), timed warm (C-side total_ms, best of 3): into pinned
+    memory (rt_host_alloc — what the NIF hands the BEAM as a resource binary) and into fresh
+    pageable memory; plus raytrace/5 natively (render + P3 text on the GPU + file)."""
+    import numpy as np
+
+    from eraytracer_amd.raytracer import render, render_ppm_file
+    out = {}
+    dt = np.float32 if args.precision == "f32" else np.float64
+    frame_px = W * H
+    pinned = N.pinned_empty((H, W, 3), dt)
+    for name, dst in (("boundary_mpx_s", pinned), ("boundary_pageable_mpx_s", None)):
+        ts = []
+        for i in range(4):
+            st = {}
+            render(W, H, scene, args.depth, precision=args.precision, order=args.order, stats=st, spp=args.spp,
+                   seed=args.seed, out=dst)
+            if i:
+                ts.append(st["total_ms"])
+        out[name] = round(frame_px / (min(ts) / 1e3) / 1e6, 3)
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "frame.ppm")
+        render_ppm_file(W, H, scene, args.depth, path, spp=args.spp, seed=args.seed)  # warm
+        tp = []
+        for _ in range(3):
+            t1 = time.perf_counter()
+            render_ppm_file(W, H, scene, args.depth, path, spp=args.spp, seed=args.seed)
+            tp.append(time.perf_counter() - t1)
+        out["p3_file_mpx_s"] = round(frame_px / min(tp) / 1e6, 3)
+        out["p3_file_bytes"] = os.path.getsize(path)
+    return out
 
 
 if __name__ == "__main__":

@@ -14,7 +14,7 @@ import ctypes
 import os
 
 from .records import tag
-from .terms import exact_eq
+from .terms import exact_key
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_LIB_PATH") or os.path.join(HERE, "librtmi355x.so")  # override: A/B builds
@@ -27,6 +27,8 @@ RT_ORDER_EXACT, RT_ORDER_FAST = 0, 1
 RT_MAX_DEPTH = 16
 RT_MAX_SHARDS = 64
 RT_CFG_SIDE_STREAMS = 1
+RT_CFG_KERNEL_TIMING = 2
+RT_KT_PRIMARY, RT_KT_LEVEL1, RT_KT_RENDER = 1, 2, 4
 
 # every symbol include/rt_mi355x.h declares (tests/test_boundary.py checks the export list)
 EXPORTS = (
@@ -34,6 +36,7 @@ EXPORTS = (
     "rt_render", "rt_prepare", "rt_shard_rows", "rt_launch", "rt_launch_spp", "rt_unshard", "rt_configure", "rt_release",
     "rt_ppm_bound", "rt_ppm_format", "rt_render_ppm_file",
     "rt_slab_header_bytes", "rt_slab_pack", "rt_slab_unpack", "rt_selftest_math",
+    "rt_host_alloc", "rt_host_free", "rt_reset_contexts", "rt_kernel_time",
 )
 
 
@@ -79,13 +82,13 @@ class RtElem(ctypes.Structure):
 class RtOpts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("first_dev", ctypes.c_int32), ("ndev", ctypes.c_int32),
                 ("precision", ctypes.c_int32), ("order", ctypes.c_int32), ("row_block", ctypes.c_uint32),
-                ("out_levels", ctypes.c_void_p), ("spp", ctypes.c_uint32), ("reserved0", ctypes.c_uint32),
+                ("out_levels", ctypes.c_void_p), ("spp", ctypes.c_uint32), ("nshards", ctypes.c_uint32),
                 ("seed", ctypes.c_uint64)]
 
 
 class RtStats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("pixels", ctypes.c_uint64),
-                ("ndev", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("ndev", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
 class RtError(RuntimeError):
@@ -139,6 +142,11 @@ def lib() -> ctypes.CDLL:
     L.rt_slab_header_bytes.argtypes = [u32, u32, u32, u32]
     L.rt_slab_pack.argtypes = [vp, u32, u32, u32, u32, u32, i32, vp, vp, vp]
     L.rt_slab_unpack.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), u32, u32, u32, u32, i32, vp, vp]
+    L.rt_host_alloc.restype = vp
+    L.rt_host_alloc.argtypes = [ctypes.c_size_t]
+    L.rt_host_free.argtypes = [vp]
+    L.rt_reset_contexts.restype = i32
+    L.rt_kernel_time.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64), i32]
     _LIB = L
     return L
 
@@ -151,6 +159,32 @@ def check(code: int, what: str = "") -> int:
     if code < 0:
         raise RtError(code, what)
     return code
+
+
+class _Pinned:
+    """Owner of one rt_host_alloc block (freed when the last array viewing it goes away)."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = lib().rt_host_alloc(nbytes)
+        if not self.ptr:
+            raise MemoryError(f"rt_host_alloc({nbytes}) failed")
+        self.nbytes = nbytes
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _LIB is not None:
+            _LIB.rt_host_free(self.ptr)
+            self.ptr = None
+
+
+def pinned_empty(shape, dtype):
+    """A numpy array in pinned host memory (rt_host_alloc): rt_render writes it by DMA."""
+    import numpy as np
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) * dt.itemsize
+    owner = _Pinned(max(n, 1))
+    buf = (ctypes.c_char * max(n, 1)).from_address(owner.ptr)
+    buf._owner = owner  # keeps the block alive while the array exists
+    return np.frombuffer(buf, dtype=dt, count=int(np.prod(shape))).reshape(shape)
 
 
 # ---- marshalling ------------------------------------------------------------------------
@@ -183,6 +217,7 @@ def marshal(scene) -> "ctypes.Array[RtElem]":
         raise ValueError("badarg: the scene must be a non-empty list whose head is a #camera{}")
     n = len(scene)
     arr = (RtElem * n)()
+    first = {}  # exact_key -> index of the first element =:= to it
     for i, t in enumerate(scene):
         e = arr[i]
         k = tag(t)
@@ -222,11 +257,7 @@ def marshal(scene) -> "ctypes.Array[RtElem]":
                 raise ValueError("badarg: the scene's first element must be a #camera{} (raytracer.erl:180)")
             e.kind = RT_OTHER
         # canon: first element exactly equal (=:=) to this one
-        e.canon = i
-        for j in range(i):
-            if arr[j].canon == j and exact_eq(scene[j], t):
-                e.canon = j
-                break
+        e.canon = first.setdefault(exact_key(t), i)
     if arr[0].kind != RT_CAMERA:
         raise ValueError("badarg: the scene's first element must be a #camera{} (raytracer.erl:180)")
     return arr

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/rt_mi355x.h"
+#include "rt_internal.h"
 
 namespace {
 
@@ -321,27 +322,26 @@ int rt_render_ppm_file(const rt_elem *scene, uint32_t n, uint32_t width, uint32_
     }
     int prev = -1;
     (void)hipGetDevice(&prev);
-    rt_prepared *p = nullptr;
-    rc = rt_prepare(scene, n, o.first_dev, &p);
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || o.first_dev < 0 || o.first_dev >= nd) return RT_ENODEV;
+    // the process's render context for this device (rt_host.hip): scene, streams, frame and text
+    // buffers and the pinned host buffer persist across calls
+    rt_ctx *ctx = nullptr;
+    rc = rt_ctx_acquire(o.first_dev, scene, n, &ctx);
     if (rc != RT_OK) return rc;
     (void)hipSetDevice(o.first_dev);
     const size_t frame_bytes = (size_t)width * height * 3 * sizeof(double);
     const size_t cap = rt_ppm_bound(width, height, max_value);
-    void *d_rgb = nullptr;
-    char *d_text = nullptr;
-    hipStream_t st = nullptr;
-    std::vector<char> text;
+    void *d_rgb = nullptr, *d_text = nullptr, *h_text = nullptr;
+    hipStream_t st = rt_ctx_stream(ctx);
     size_t len = 0;
     do {
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { rc = RT_EHIP; break; }
-        if (hipMalloc(&d_rgb, frame_bytes) != hipSuccess || hipMalloc(reinterpret_cast<void **>(&d_text), cap) != hipSuccess) {
-            rc = RT_ENOMEM;
-            break;
-        }
-        rc = rt_launch_spp(p, width, height, depth, o.row_block, 0, 1, RT_OUT_F64, o.order, o.spp, o.seed, d_rgb,
-                           nullptr, st);
+        if ((rc = rt_ctx_device_buffer(ctx, 0, frame_bytes, &d_rgb)) != RT_OK) break;
+        if ((rc = rt_ctx_device_buffer(ctx, 2, cap, &d_text)) != RT_OK) break;
+        rc = rt_launch_spp(rt_ctx_prepared(ctx), width, height, depth, o.row_block, 0, 1, RT_OUT_F64, o.order, o.spp,
+                           o.seed, d_rgb, nullptr, st);
         if (rc != RT_OK) break;
-        rc = rt_ppm_format(d_rgb, RT_OUT_F64, width, height, max_value, d_text, cap, &len, st);
+        rc = rt_ppm_format(d_rgb, RT_OUT_F64, width, height, max_value, static_cast<char *>(d_text), cap, &len, st);
         if (rc == RT_ERANGE) { // a colour BEAM would print as a bignum: format on the host
             std::vector<double> img((size_t)width * height * 3);
             if (hipMemcpy(img.data(), d_rgb, frame_bytes, hipMemcpyDeviceToHost) != hipSuccess) { rc = RT_EHIP; break; }
@@ -351,17 +351,17 @@ int rt_render_ppm_file(const rt_elem *scene, uint32_t n, uint32_t width, uint32_
             break;
         }
         if (rc != RT_OK) break;
-        text.resize(len);
-        if (hipMemcpy(text.data(), d_text, len, hipMemcpyDeviceToHost) != hipSuccess) { rc = RT_EHIP; break; }
+        // the text to pinned memory by DMA, written to the file from there
+        if ((rc = rt_ctx_host_buffer(ctx, len ? len : 1, &h_text)) != RT_OK) break;
+        if (hipMemcpyAsync(h_text, d_text, len, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) { rc = RT_EHIP; break; }
         f = std::fopen(path, "wb");
         if (!f) { rc = RT_EBADARG; break; }
-        if (std::fwrite(text.data(), 1, len, f) != len) rc = RT_EBADARG;
+        if (std::fwrite(h_text, 1, len, f) != len) rc = RT_EBADARG;
     } while (0);
     if (f) std::fclose(f);
-    if (d_rgb) (void)hipFree(d_rgb);
-    if (d_text) (void)hipFree(d_text);
-    if (st) (void)hipStreamDestroy(st);
-    rt_release(p);
+    (void)hipStreamSynchronize(st);
+    rt_ctx_release(ctx);
     if (prev >= 0) (void)hipSetDevice(prev);
     if (stats && rc == RT_OK) {
         stats->pixels = (uint64_t)width * height;

@@ -38,6 +38,7 @@
 
 #include "../../include/rt_mi355x.h"
 #include "rt_layout.h"
+#include "rt_internal.h"
 #include "rt_scene.h"
 
 using namespace rtl;
@@ -877,16 +878,17 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
 template <int ORDER, int PREC, bool LEVELS, bool GENPOW>
 __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict__ tab,
                                                   const int *__restrict__ itab, int W, int H, int depth, int rb,
-                                                  int shard, int nshards, int slab_rows, void *__restrict__ out,
+                                                  int shard, int nshards, int row0, int row_end, void *__restrict__ out,
                                                   uint8_t *__restrict__ levels) {
+    // this launch covers slab rows [row0, row_end); out / levels point at slab row 0
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Scene S{hdr, tab, itab};
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int x = blockIdx.x * TILE + (wave & 1) * 8 + (lane & 7);
-    const int ly = blockIdx.y * TILE + (wave >> 1) * 8 + (lane >> 3);
-    const bool inside = x < W && ly < slab_rows;
+    const int ly = row0 + blockIdx.y * TILE + (wave >> 1) * 8 + (lane >> 3);
+    const bool inside = x < W && ly < row_end;
     // slab row -> image row: the tile's first row split once (wave-uniform), the offset (< 16) added
-    const int ly_base = blockIdx.y * TILE, q_base = ly_base / rb;
+    const int ly_base = row0 + blockIdx.y * TILE, q_base = ly_base / rb;
     int rr = ly_base - q_base * rb + (ly - ly_base), qq = q_base;
     while (rr >= rb) {
         rr -= rb;
@@ -1065,6 +1067,15 @@ struct rt_prepared {
     // rt_launch captures the frame's launch sequence into a graph, later ones replay it.
     // gen counts work-space reallocations, which invalidate captured pointers.
     unsigned gen = 0;
+    // RT_CFG_KERNEL_TIMING: per timed kernel (RT_KT_* bit i), a ring of event pairs; a full ring
+    // folds its oldest pair into the sum (waiting for it)
+    int timing_mask = 0;
+    struct KTimer {
+        std::vector<hipEvent_t> a, b;
+        size_t head = 0, n = 0;
+        double sum_ms = 0;
+        unsigned long long count = 0;
+    } kt[3];
     hipStream_t cap = nullptr;
     hipGraphExec_t gexec = nullptr;
     long long gkey[12] = {};
@@ -1094,17 +1105,54 @@ struct DevGuard { // restore the caller's current device on scope exit
     }
 };
 
+constexpr size_t KT_RING = 64;
+int kt_index(int kernel) { return kernel == RT_KT_PRIMARY ? 0 : kernel == RT_KT_LEVEL1 ? 1 : kernel == RT_KT_RENDER ? 2 : -1; }
+void kt_fold_oldest(rt_prepared::KTimer &t) {
+    const size_t i = (t.head + KT_RING - t.n) % KT_RING;
+    float ms = 0;
+    if (hipEventSynchronize(t.b[i]) == hipSuccess && hipEventElapsedTime(&ms, t.a[i], t.b[i]) == hipSuccess) {
+        t.sum_ms += ms;
+        ++t.count;
+    }
+    --t.n;
+}
+// bracket one launch of `kernel` (an RT_KT_* bit) on `st` when the context times it
+struct KtScope {
+    rt_prepared::KTimer *t = nullptr;
+    hipStream_t st;
+    KtScope(rt_prepared *p, int kernel, hipStream_t s) : st(s) {
+        if (!(p->timing_mask & kernel)) return;
+        rt_prepared::KTimer &k = p->kt[kt_index(kernel)];
+        if (k.a.empty()) {
+            k.a.resize(KT_RING);
+            k.b.resize(KT_RING);
+            for (size_t i = 0; i < KT_RING; ++i)
+                if (hipEventCreate(&k.a[i]) != hipSuccess || hipEventCreate(&k.b[i]) != hipSuccess) return;
+        }
+        if (k.n == KT_RING) kt_fold_oldest(k);
+        if (hipEventRecord(k.a[k.head], st) != hipSuccess) return;
+        t = &k;
+    }
+    ~KtScope() {
+        if (!t) return;
+        (void)hipEventRecord(t->b[t->head], st);
+        t->head = (t->head + 1) % KT_RING;
+        ++t->n;
+    }
+};
+
 template <int ORDER, int PREC, bool GENPOW>
-int launch_t(const rt_prepared *p, int W, int H, int depth, int rb, int shard, int nshards, int slab_rows, void *out,
-             uint8_t *levels, hipStream_t st) {
-    dim3 grid((W + TILE - 1) / TILE, (slab_rows + TILE - 1) / TILE);
+int launch_t(rt_prepared *p, int W, int H, int depth, int rb, int shard, int nshards, int row0, int row_end,
+             void *out, uint8_t *levels, hipStream_t st) {
+    dim3 grid((W + TILE - 1) / TILE, (row_end - row0 + TILE - 1) / TILE);
     size_t lds = ORDER == RT_ORDER_EXACT ? (size_t)depth * BLOCK * 12 : 0;
+    KtScope kt(p, RT_KT_RENDER, st);
     if (levels)
         hipLaunchKernelGGL((k_render<ORDER, PREC, true, GENPOW>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
-                           H, depth, rb, shard, nshards, slab_rows, out, levels);
+                           H, depth, rb, shard, nshards, row0, row_end, out, levels);
     else
         hipLaunchKernelGGL((k_render<ORDER, PREC, false, GENPOW>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
-                           H, depth, rb, shard, nshards, slab_rows, out, levels);
+                           H, depth, rb, shard, nshards, row0, row_end, out, levels);
     HIPCHK(hipGetLastError());
     return RT_OK;
 }
@@ -1216,6 +1264,39 @@ int rt_prepare(const rt_elem *scene, uint32_t n, int device, rt_prepared **out) 
     return RT_OK;
 }
 
+} // extern "C"
+
+int rt_prepare_scene(rt_prepared *p, const rt_elem *scene, uint32_t n) {
+    if (!p) return RT_EBADARG;
+    Compiled c;
+    int rc = compile_scene(scene, n, c);
+    if (rc != RT_OK) return rc;
+    DevGuard g(p->device);
+    double *tab = nullptr;
+    int *itab = nullptr;
+    if (hipMalloc(&tab, c.tab.size() * sizeof(double)) != hipSuccess) return RT_ENOMEM;
+    if (hipMalloc(&itab, c.itab.size() * sizeof(int)) != hipSuccess) {
+        (void)hipFree(tab);
+        return RT_ENOMEM;
+    }
+    if (hipMemcpy(tab, c.tab.data(), c.tab.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(itab, c.itab.data(), c.itab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(tab);
+        (void)hipFree(itab);
+        return RT_EHIP;
+    }
+    (void)hipFree(p->d_tab);
+    (void)hipFree(p->d_itab);
+    p->d_tab = tab;
+    p->d_itab = itab;
+    p->hdr = c.hdr;
+    ++p->gen; // captured graphs hold the old tables
+    p->last_valid = false;
+    return RT_OK;
+}
+
+extern "C" {
+
 int rt_configure(rt_prepared *p, int option, int64_t value) {
     if (!p) return RT_EBADARG;
     switch (option) {
@@ -1223,9 +1304,33 @@ int rt_configure(rt_prepared *p, int option, int64_t value) {
         if (value < -1 || value > 1) return RT_EBADARG;
         p->side_mode = (int)value;
         return RT_OK;
+    case RT_CFG_KERNEL_TIMING:
+        if (value < 0 || value > 7) return RT_EBADARG;
+        p->timing_mask = (int)value;
+        return RT_OK;
     default:
         return RT_EBADARG;
     }
+}
+
+} // extern "C"
+
+
+extern "C" {
+
+int rt_kernel_time(rt_prepared *p, int kernel, double *total_ms, uint64_t *launches, int reset) {
+    const int i = p ? kt_index(kernel) : -1;
+    if (i < 0) return RT_EBADARG;
+    DevGuard g(p->device);
+    rt_prepared::KTimer &t = p->kt[i];
+    while (t.n) kt_fold_oldest(t);
+    if (total_ms) *total_ms = t.sum_ms;
+    if (launches) *launches = t.count;
+    if (reset) {
+        t.sum_ms = 0;
+        t.count = 0;
+    }
+    return RT_OK;
 }
 
 int rt_release(rt_prepared *p) {
@@ -1248,6 +1353,10 @@ int rt_release(rt_prepared *p) {
         if (x) (void)hipStreamDestroy(x);
     if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
     if (p->cap) (void)hipStreamDestroy(p->cap);
+    for (auto &t : p->kt) {
+        for (hipEvent_t e : t.a) (void)hipEventDestroy(e);
+        for (hipEvent_t e : t.b) (void)hipEventDestroy(e);
+    }
     delete p;
     return RT_OK;
 }
@@ -1302,8 +1411,10 @@ int grow(void **buf, size_t *have, size_t need, unsigned *gen) {
 }
 
 template <int PREC, bool GENPOW>
-int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns, int slab_rows, void *out,
+int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns, int row_begin, int row_end, void *out,
                      uint8_t *levels, hipStream_t st, int spp = 1, int sample = 0, unsigned long long seed = 0) {
+    // renders slab rows [row_begin, row_end) (row_begin a multiple of TILE); out / levels point at slab row 0
+    const int slab_rows = row_end - row_begin;
     const int nlev = D > 0 ? D : 1;
     const size_t per_row = (size_t)W * nlev * sizeof(HitRec);
     int pass_rows = (int)std::min<size_t>((size_t)slab_rows, std::max<size_t>(TILE, queue_budget() / per_row));
@@ -1345,8 +1456,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         return !(e && std::strcmp(e, "0") == 0);
     }();
     const bool fuse = fuse_env && !overlap && !levels && nrefl > 0;
-    for (int row0 = 0; row0 < slab_rows; row0 += pass_rows) {
-        const int rows = std::min(pass_rows, slab_rows - row0);
+    for (int row0 = row_begin; row0 < row_end; row0 += pass_rows) {
+        const int rows = std::min(pass_rows, row_end - row0);
         const int ntiles = tiles_x * ((rows + TILE - 1) / TILE);
         // the pass covers slab rows [row0, row0 + rows): out/levels offset to row0; the
         // kernels map slab rows to image rows through the shard interleave themselves
@@ -1363,12 +1474,15 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
         dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
-        if (lv)
-            hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H, D,
-                               rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed);
-        else
-            hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W, H,
-                               D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed);
+        {
+            KtScope kt(p, RT_KT_PRIMARY, st);
+            if (lv)
+                hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W,
+                                   H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed);
+            else
+                hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
+                                   W, H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed);
+        }
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
         // level k's dense list, then its shading (k_light reads only level k: on a side stream
@@ -1398,6 +1512,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         for (int k = 1; k <= nrefl; ++k) {
             // level 1 (from the primary hits) is dense and throughput-bound; deeper levels are a few
             // waves each, bound by one wave's dependent chain: they walk two candidates per step
+            KtScope kt(p, k == 1 ? RT_KT_LEVEL1 : 0, st);
             if (fuse) {
 #define RT_RS(SPHV, ILPV)                                                                                           \
     hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, \
@@ -1563,6 +1678,18 @@ int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, u
 int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, uint32_t row_block,
                   uint32_t shard, uint32_t nshards, int precision, int order, uint32_t spp, uint64_t seed,
                   void *d_out, uint8_t *d_levels, void *stream) {
+    return rt_launch_rows(p, width, height, depth, row_block, shard, nshards, precision, order, spp, seed, 0, ~0u,
+                          d_out, d_levels, stream);
+}
+
+} // extern "C"
+
+// rt_launch_spp restricted to slab rows [row_begin, min(row_end, slab rows)): the boundary
+// (rt_host.hip) renders a frame in row bands so that each band's copy to the host overlaps
+// the next band's render.  row_begin must be a multiple of 16 (the tile height).
+int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, uint32_t row_block,
+                   uint32_t shard, uint32_t nshards, int precision, int order, uint32_t spp, uint64_t seed,
+                   uint32_t row_begin, uint32_t row_end, void *d_out, uint8_t *d_levels, void *stream) {
     if (!p || !d_out) return RT_EBADARG;
     if (width == 0 && height == 0) return RT_DONE;
     if (width == 0 || height == 0) return RT_EBADARG;
@@ -1575,10 +1702,13 @@ int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dept
     if (width > (1u << 20) || height > (1u << 20)) return RT_ETOOBIG;
     uint32_t slab = rt_shard_rows(height, row_block, nshards);
     if ((uint64_t)slab > 65535ull * TILE) return RT_ETOOBIG;
+    if (row_begin % TILE) return RT_EBADARG;
+    if (row_end > slab) row_end = slab;
+    if (row_begin >= row_end) return RT_OK;
     DevGuard g(p->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     int W = (int)width, H = (int)height, D = (int)depth, rb = (int)row_block, sh = (int)shard, ns = (int)nshards;
-    const int slab_rows = (int)slab;
+    const int r0 = (int)row_begin, r1 = (int)row_end, slab_rows = (int)slab;
     if (spp > 1) { // RT_SUPERSAMPLING, on the wavefront engine: one pass per sample, summed in order
         // the slab rows inside the image (a prefix: global rows grow with slab rows)
         size_t valid_rows = 0;
@@ -1586,43 +1716,47 @@ int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dept
             const long long base = ((long long)blk * ns + sh) * rb;
             valid_rows += (size_t)std::max(0LL, std::min((long long)rb, (long long)H - base));
         }
-        const size_t n = valid_rows * W * 3;
-        if (n == 0) return RT_OK;
+        const size_t v1 = std::min<size_t>(valid_rows, (size_t)r1);
+        if (v1 <= (size_t)r0) return RT_OK;
+        const size_t e0 = (size_t)r0 * W * 3, n = (v1 - r0) * W * 3; // the band's elements
         const size_t n_slab = (size_t)slab_rows * W * 3;
         int rc = grow(reinterpret_cast<void **>(&p->d_sample), &p->sample_bytes, 2 * n_slab * sizeof(double), &p->gen);
         if (rc != RT_OK) return rc;
         double *smp = p->d_sample, *acc = p->d_sample + n_slab;
         const int blocks = (int)std::min<size_t>(8192, (n + 255) / 256);
+        void *dst = static_cast<char *>(d_out) + e0 * (precision == RT_OUT_F64 ? 8 : 4);
         for (int s = 0; s < (int)spp; ++s) {
-            rc = p->hdr.int_pow ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, slab_rows, smp,
+            rc = p->hdr.int_pow ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, r0, r1, smp,
                                                                       s == 0 ? d_levels : nullptr, st, (int)spp, s, seed)
-                                : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, slab_rows, smp,
+                                : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, r0, r1, smp,
                                                                      s == 0 ? d_levels : nullptr, st, (int)spp, s, seed);
             if (rc != RT_OK) return rc;
             if (precision == RT_OUT_F64)
-                hipLaunchKernelGGL(k_accum<RT_OUT_F64>, dim3(blocks), dim3(256), 0, st, n, smp, acc, d_out, s, (int)spp);
+                hipLaunchKernelGGL(k_accum<RT_OUT_F64>, dim3(blocks), dim3(256), 0, st, n, smp + e0, acc + e0, dst, s,
+                                   (int)spp);
             else
-                hipLaunchKernelGGL(k_accum<RT_OUT_F32>, dim3(blocks), dim3(256), 0, st, n, smp, acc, d_out, s, (int)spp);
+                hipLaunchKernelGGL(k_accum<RT_OUT_F32>, dim3(blocks), dim3(256), 0, st, n, smp + e0, acc + e0, dst, s,
+                                   (int)spp);
             HIPCHK(hipGetLastError());
         }
         return RT_OK;
     }
     if (!use_mega_engine(p)) { // the wavefront engine always evaluates the reference's exact order
-        const long long key[12] = {W, H, D, rb, sh, ns, precision, slab_rows, (long long)(intptr_t)d_out,
-                                   (long long)(intptr_t)d_levels, 0, 0};
+        const long long key[12] = {W, H, D, rb, sh, ns, precision, ((long long)r0 << 32) | r1,
+                                   (long long)(intptr_t)d_out, (long long)(intptr_t)d_levels, 0, 0};
         return launch_frame(p, key, st, [&](hipStream_t s) {
             if (precision == RT_OUT_F64)
                 return p->hdr.int_pow
-                           ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, s)
-                           : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, s);
+                           ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s)
+                           : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s);
             return p->hdr.int_pow
-                       ? launch_wavefront<RT_OUT_F32, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, s)
-                       : launch_wavefront<RT_OUT_F32, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, s);
+                       ? launch_wavefront<RT_OUT_F32, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s)
+                       : launch_wavefront<RT_OUT_F32, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s);
         });
     }
 #define RT_DISPATCH(O, P)                                                                                          \
-    return p->hdr.int_pow ? launch_t<O, P, false>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)           \
-                          : launch_t<O, P, true>(p, W, H, D, rb, sh, ns, slab_rows, d_out, d_levels, st)
+    return p->hdr.int_pow ? launch_t<O, P, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, st)              \
+                          : launch_t<O, P, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, st)
     if (order == RT_ORDER_EXACT) {
         if (precision == RT_OUT_F64) RT_DISPATCH(RT_ORDER_EXACT, RT_OUT_F64);
         RT_DISPATCH(RT_ORDER_EXACT, RT_OUT_F32);
@@ -1631,6 +1765,8 @@ int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dept
     RT_DISPATCH(RT_ORDER_FAST, RT_OUT_F32);
 #undef RT_DISPATCH
 }
+
+extern "C" {
 
 // Copy the blocks of one shard's slab to their rows in a row-major image.  dst_kind selects
 // hipMemcpyDeviceToDevice or DeviceToHost.
@@ -1663,99 +1799,6 @@ int rt_unshard(const void *d_slabs, uint32_t width, uint32_t height, uint32_t ro
         if (rc != RT_OK) return rc;
     }
     return RT_OK;
-}
-
-int rt_render(const rt_elem *scene, uint32_t n, uint32_t width, uint32_t height, uint32_t depth,
-              const rt_opts *opts, void *out_rgb, rt_stats *stats) {
-    auto t_begin = std::chrono::steady_clock::now();
-    if (width == 0 && height == 0) return RT_DONE;
-    if (width == 0 || height == 0) return RT_EBADARG;
-    if (!out_rgb) return RT_EBADARG;
-    if (depth > RT_MAX_DEPTH) return RT_ETOOBIG;
-    rt_opts o;
-    std::memset(&o, 0, sizeof(o));
-    o.ndev = 1;
-    o.row_block = 16;
-    o.spp = 1;
-    if (opts && opts->struct_size) {
-        std::memcpy(&o, opts, opts->struct_size < sizeof(o) ? opts->struct_size : sizeof(o));
-        if (o.row_block == 0) o.row_block = 16;
-        if (o.ndev == 0) o.ndev = 1;
-        if (opts->struct_size < offsetof(rt_opts, spp) + sizeof(o.spp) || o.spp == 0) o.spp = 1; // ABI 1 callers
-    }
-    int rc = check_scene(scene, n);
-    if (rc != RT_OK) return rc;
-    int navail = 0;
-    if (hipGetDeviceCount(&navail) != hipSuccess || navail <= 0) return RT_ENODEV;
-    if (o.ndev < 0) o.ndev = navail - o.first_dev;
-    if (o.first_dev < 0 || o.ndev <= 0 || o.first_dev + o.ndev > navail) return RT_ENODEV;
-    const uint32_t ns = (uint32_t)o.ndev, rb = o.row_block;
-    const uint32_t slab = rt_shard_rows(height, rb, ns);
-    const size_t esz = o.precision == RT_OUT_F32 ? 4 : 8;
-    const uint32_t rowbytes = width * 3 * (uint32_t)esz;
-
-    struct Dev {
-        rt_prepared *p = nullptr;
-        void *d_out = nullptr;
-        uint8_t *d_lv = nullptr;
-        hipStream_t st = nullptr;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-    };
-    std::vector<Dev> devs(ns);
-    int err = RT_OK;
-    for (uint32_t s = 0; s < ns && err == RT_OK; s++) {
-        Dev &dv = devs[s];
-        int dev = o.first_dev + (int)s;
-        err = rt_prepare(scene, n, dev, &dv.p);
-        if (err != RT_OK) break;
-        DevGuard g(dev);
-        if (hipStreamCreateWithFlags(&dv.st, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreate(&dv.e0) != hipSuccess || hipEventCreate(&dv.e1) != hipSuccess) {
-            err = RT_EHIP;
-            break;
-        }
-        if (hipMalloc(&dv.d_out, (size_t)slab * rowbytes) != hipSuccess ||
-            (o.out_levels && hipMalloc((void **)&dv.d_lv, (size_t)slab * width) != hipSuccess)) {
-            err = RT_ENOMEM;
-            break;
-        }
-        (void)hipEventRecord(dv.e0, dv.st);
-        err = rt_launch_spp(dv.p, width, height, depth, rb, s, ns, o.precision, o.order, o.spp, o.seed, dv.d_out,
-                            dv.d_lv, dv.st);
-        if (err != RT_OK) break;
-        (void)hipEventRecord(dv.e1, dv.st);
-        err = scatter_slab(static_cast<const char *>(dv.d_out), rowbytes, height, rb, s, ns,
-                           static_cast<char *>(out_rgb), hipMemcpyDeviceToHost, dv.st);
-        if (err == RT_OK && o.out_levels)
-            err = scatter_slab(reinterpret_cast<const char *>(dv.d_lv), width, height, rb, s, ns,
-                               reinterpret_cast<char *>(o.out_levels), hipMemcpyDeviceToHost, dv.st);
-    }
-    double kms = 0;
-    for (uint32_t s = 0; s < ns; s++) {
-        Dev &dv = devs[s];
-        if (!dv.p) continue;
-        DevGuard g(dv.p->device);
-        if (dv.st) {
-            if (hipStreamSynchronize(dv.st) != hipSuccess && err == RT_OK) err = RT_EHIP;
-            float ms = 0;
-            if (err == RT_OK && hipEventElapsedTime(&ms, dv.e0, dv.e1) == hipSuccess && ms > kms) kms = ms;
-        }
-        if (dv.e0) (void)hipEventDestroy(dv.e0);
-        if (dv.e1) (void)hipEventDestroy(dv.e1);
-        if (dv.st) (void)hipStreamDestroy(dv.st);
-        if (dv.d_out) (void)hipFree(dv.d_out);
-        if (dv.d_lv) (void)hipFree(dv.d_lv);
-        rt_release(dv.p);
-    }
-    if (stats) {
-        stats->kernel_ms = kms;
-        stats->total_ms =
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count();
-        stats->pixels = (uint64_t)width * height;
-        stats->ndev = (int32_t)ns;
-        stats->reserved = 0;
-    }
-    return err;
 }
 
 } // extern "C"

@@ -276,6 +276,41 @@ class CompactGather:
         return self.frame if self.rank == 0 else None
 
 
+def verify_compact_gather(cg, make_slab, reference, rank, nframes=2):
+    """The multi-rank bench's self-check before timing: every rank renders its slab of a check
+    frame (``make_slab(i)``, frame i), the slabs go through the compact gather ``cg`` exactly as
+    in the timed loop (frames in flight), and rank 0 compares every reassembled frame bit for
+    bit with ``reference(i)`` (a one-shard render of the same frame).  Raises on a mismatch;
+    returns the number of frames checked on rank 0 (0 elsewhere)."""
+    import torch
+    got = []
+
+    def keep(f):
+        if cg.frame_ready is not None:
+            torch.cuda.current_stream().wait_event(cg.frame_ready)
+        got.append(f.clone())
+        if cg.cuda:
+            torch.cuda.synchronize()
+
+    for i in range(nframes):
+        out = cg.submit(make_slab(i), rank)
+        if out is not None:
+            keep(out)
+    cg.drain(on_frame=keep)
+    if rank != 0:
+        return 0
+    if len(got) != nframes:
+        raise RuntimeError(f"compact gather returned {len(got)} of {nframes} frames")
+    for i, f in enumerate(got):
+        ref = reference(i)
+        a = f.contiguous().view(torch.int32 if f.dtype == torch.float32 else torch.int64)
+        b = ref.to(f.device).contiguous().view(a.dtype)
+        if not torch.equal(a, b):
+            bad = int((a != b).any(-1).sum())
+            raise RuntimeError(f"gathered frame {i} differs from the one-shard frame in {bad} pixels")
+    return nframes
+
+
 class FrameRenderer:
     """Renders this rank's rows of a W x H frame on its GPU and gathers the frame to rank 0.
 
@@ -344,6 +379,32 @@ class FrameRenderer:
         N.check(self.L.rt_launch_spp(self._ps[j], self.w, self.h, self.depth, self.rb, self.rank, self.world, self.prec,
                                      self.order, self.spp, self.seed, self.slab.data_ptr(), lv,
                                      self.stream.cuda_stream), "rt_launch")
+
+    def launch_on(self, j: int):
+        """Render a frame on slot j's context, slab and stream (no gather)."""
+        stream = self.streams[j] if self.streams is not None else self.torch.cuda.current_stream(self.device)
+        N.check(self.L.rt_launch_spp(self._ps[j], self.w, self.h, self.depth, self.rb, self.rank, self.world, self.prec,
+                                     self.order, self.spp, self.seed, self.slabs[j].data_ptr(), None,
+                                     stream.cuda_stream), "rt_launch")
+
+    def time_kernels(self, mask: int):
+        """Bracket every later launch of the RT_KT_* kernels in `mask` with HIP events on the
+        stream each runs on (every slot context); 0 stops."""
+        for p in self._ps:
+            N.check(self.L.rt_configure(p, N.RT_CFG_KERNEL_TIMING, mask), "rt_configure")
+            for k in (N.RT_KT_PRIMARY, N.RT_KT_LEVEL1, N.RT_KT_RENDER):
+                N.check(self.L.rt_kernel_time(p, k, None, None, 1), "rt_kernel_time")  # reset
+
+    def kernel_time(self, kernel: int):
+        """(average ms per launch, launches) of an RT_KT_* kernel over every slot context since
+        time_kernels(); waits for the recorded events."""
+        tot, n = 0.0, 0
+        for p in self._ps:
+            ms, c = ctypes.c_double(0), ctypes.c_uint64(0)
+            N.check(self.L.rt_kernel_time(p, kernel, ctypes.byref(ms), ctypes.byref(c), 0), "rt_kernel_time")
+            tot += ms.value
+            n += c.value
+        return (tot / n if n else None), n
 
     def fork(self):
         """Make every slot stream wait for the caller's current stream (start of a timed region)."""

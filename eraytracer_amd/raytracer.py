@@ -54,9 +54,13 @@ def _depth_ok(depth):
 
 def render(width: int, height: int, scene=None, depth: int = 5, *, precision: str = "f64",
            order: str = "exact", ndev: int = 1, first_dev: int = 0, row_block: int = 16,
-           levels: bool = False, stats: dict | None = None, spp: int = 1, seed: int = 0):
+           levels: bool = False, stats: dict | None = None, spp: int = 1, seed: int = 0, out=None,
+           nshards: int = 0):
     """Render through ``rt_render`` and return a ``(height, width, 3)`` array (float64 or
     float32), plus the per-pixel levels array if ``levels``.  ``'done'`` for 0x0.
+    ``out``: an existing C-contiguous array of that shape and dtype to render into (e.g.
+    ``_native.pinned_empty``: pinned memory is written by DMA directly).  ``nshards``: row
+    shards of the distributed split (default one per device; shard s on device s % ndev).
     ``spp`` > 1: stochastic supersampling as defined at RT_SUPERSAMPLING in
     include/rt_mi355x.h (not in the reference; levels then report sample 0)."""
     if not _sizes_ok(width, height):
@@ -68,53 +72,69 @@ def render(width: int, height: int, scene=None, depth: int = 5, *, precision: st
     L = N.lib()
     prec = {"f64": N.RT_OUT_F64, "f32": N.RT_OUT_F32}[precision]
     dt = np.float64 if prec == N.RT_OUT_F64 else np.float32
-    out = np.empty((height, width, 3), dtype=dt)
+    if out is None:
+        out = np.empty((height, width, 3), dtype=dt)
+    elif out.shape != (height, width, 3) or out.dtype != dt or not out.flags.c_contiguous:
+        raise ValueError(f"out must be a C-contiguous {(height, width, 3)} {np.dtype(dt).name} array")
     lv = np.empty((height, width), dtype=np.uint8) if levels else None
     opts = N.RtOpts(ctypes.sizeof(N.RtOpts), first_dev, ndev, prec,
                     {"exact": N.RT_ORDER_EXACT, "fast": N.RT_ORDER_FAST}[order], row_block,
-                    lv.ctypes.data if levels else None, spp, 0, seed)
+                    lv.ctypes.data if levels else None, spp, nshards, seed)
     st = N.RtStats()
     rc = L.rt_render(elems, len(elems), width, height, depth, ctypes.byref(opts), out.ctypes.data, ctypes.byref(st))
     if rc == N.RT_DONE:
         return DONE
     N.check(rc, "rt_render")
     if stats is not None:
-        stats.update(kernel_ms=st.kernel_ms, total_ms=st.total_ms, pixels=st.pixels, ndev=st.ndev)
+        stats.update(kernel_ms=st.kernel_ms, total_ms=st.total_ms, pixels=st.pixels, ndev=st.ndev,
+                     pinned=bool(st.flags & 1))
     return (out, lv) if levels else out
 
 
-def _pixel_list(img, keyed: bool):
-    h, w, _ = img.shape
+def _has_lights(scene) -> bool:
+    from .records import tag
+    return any(tag(t) == "point_light" for t in scene)
+
+
+def _pixel_list(img, lv, scene, keyed: bool):
+    """The strategy's result list with the reference's exact term types: the integer zeros
+    #colour{r=0,g=0,b=0} where the reference returns them — no primary hit (?BACKGROUND_COLOUR,
+    raytracer.erl:82, :201), depth 0 (:186-187; levels are 0 there) or a scene without point
+    lights (lighting_function/6 folds from #vector{0,0,0}, :250) — floats everywhere else
+    (specular_term's math:pow/2 always yields a float, :289).  Keys: 1 (simple, :95) or
+    X+Y*Width (:112, :173)."""
     flat = img.reshape(-1, 3).tolist()
+    zero = (lv.reshape(-1) == 0) if _has_lights(scene) else np.ones(len(flat), dtype=bool)
+    ints = (0, 0, 0)
     if keyed:
-        return [(i, (r, g, b)) for i, (r, g, b) in enumerate(flat)]
-    return [(1, (r, g, b)) for (r, g, b) in flat]
+        return [(i, ints if z else (r, g, b)) for i, ((r, g, b), z) in enumerate(zip(flat, zero.tolist()))]
+    return [(1, ints if z else (r, g, b)) for (r, g, b), z in zip(flat, zero.tolist())]
+
+
+def _strategy(Width, Height, Scene, Recursion_depth, keyed, ndev=1):
+    if not _sizes_ok(Width, Height):
+        return DONE
+    if Scene is None:
+        Scene = default_scene()
+    img, lv = render(Width, Height, Scene, Recursion_depth, levels=True, ndev=ndev)
+    return _pixel_list(img, lv, Scene, keyed)
 
 
 def raytraced_pixel_list_simple(Width, Height, Scene, Recursion_depth):
     """raytraced_pixel_list_simple/4 (raytracer.erl:86-99): ``[{1, {R,G,B}}]`` row-major."""
-    img = render(Width, Height, Scene, Recursion_depth)
-    if isinstance(img, str):
-        return img
-    return _pixel_list(img, keyed=False)
+    return _strategy(Width, Height, Scene, Recursion_depth, keyed=False)
 
 
 def raytraced_pixel_list_concurrent(Width, Height, Scene, Recursion_depth):
     """raytraced_pixel_list_concurrent/4 (raytracer.erl:101-119): ``[{X+Y*W, {R,G,B}}]``
     sorted by key (the master's lists:keysort, :155), i.e. row-major."""
-    img = render(Width, Height, Scene, Recursion_depth)
-    if isinstance(img, str):
-        return img
-    return _pixel_list(img, keyed=True)
+    return _strategy(Width, Height, Scene, Recursion_depth, keyed=True)
 
 
 def raytraced_pixel_list_distributed(Width, Height, Scene, Recursion_depth):
     """raytraced_pixel_list_distributed/4 (raytracer.erl:121-149): the same pixels and
     keys as concurrent; rows are sharded over every GPU visible to this process."""
-    img = render(Width, Height, Scene, Recursion_depth, ndev=-1)
-    if isinstance(img, str):
-        return img
-    return _pixel_list(img, keyed=True)
+    return _strategy(Width, Height, Scene, Recursion_depth, keyed=True, ndev=-1)
 
 
 raytraced_pixel_list_gpu = raytraced_pixel_list_concurrent

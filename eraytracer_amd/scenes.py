@@ -16,7 +16,7 @@ rules: no light inside (or on) a sphere, no two spheres with the same centre and
 """
 from __future__ import annotations
 
-from .records import camera, colour, material, point_light, screen, sphere, vector
+from .records import camera, colour, material, plane, point_light, screen, sphere, triangle, vector
 
 MASK64 = (1 << 64) - 1
 SEED_S64 = 0x5EED0064
@@ -91,9 +91,51 @@ def s256():
     return synthetic_scene(256, SEED_S256)
 
 
+def default_powers(powers=(0, 0.5, 2.5, 1025)):
+    """The default scene (raytracer.erl:618-665) with its four objects' specular powers
+    replaced by ``powers`` (cycled): by default 0 (math:pow(0, 0) = 1.0 where the highlight
+    term is 0), non-integer and > 1024 exponents — the general math:pow/2 path (:289) that
+    the library compiles in only for such scenes."""
+    from .records import scene as default_scene
+    out = []
+    i = 0
+    for t in default_scene():
+        if t[0] in ("sphere", "triangle", "plane"):
+            m = t[-1]
+            t = t[:-1] + (material(m[1], powers[i % len(powers)], m[3], m[4]),)
+            i += 1
+        out.append(t)
+    return out
+
+
+def synthetic_mixed(n_spheres: int = 48, seed: int = 0x5EED0048, powers=(1, 4, 20, 0.5, 2.5, 0)):
+    """A scene for the wavefront engine's mixed-object paths (more than the fused engine's 40
+    objects): S-style spheres plus the default scene's triangle and plane, two more triangles
+    (one facing away: back-face culled, :410) and a second plane, specular powers from
+    ``powers`` (non-integer ones select the general math:pow/2 path)."""
+    base = synthetic_scene(n_spheres, seed)
+    rng = SplitMix64(seed ^ 0xA5A5)
+    out = []
+    for t in base:
+        if t[0] == "sphere":
+            m = t[3]
+            t = sphere(t[1], t[2], material(m[1], powers[rng.next_u64() % len(powers)], m[3], m[4]))
+        out.append(t)
+    out.insert(5, triangle(vector(-2, 5, 5), vector(4, 5, 10), vector(4, -5, 10),
+                           material(colour(1, 0.5, 0), 4, 0.25, 0.5)))
+    out.append(plane(vector(0, -1, 0), 5, material(colour(1, 1, 1), 1, 0, 0.01)))
+    out.append(triangle(vector(-8, -4, 20), vector(-3, 2, 22), vector(2, -4, 24),
+                        material(colour(0.25, 0.75, 0.5), 2.5, 0.5, 0.25)))
+    out.append(triangle(vector(2, -4, 24), vector(-3, 2, 22), vector(-8, -4, 20),
+                        material(colour(0.75, 0.25, 0.5), 20, 0.5, 0.25)))
+    out.append(plane(vector(1, 0, 0), 14, material(colour(0.5, 0.5, 1), 0.5, 0.25, 0.3)))
+    return out
+
+
 def named(name: str):
     from .records import scene as default_scene
-    table = {"default": default_scene, "s64": s64, "s256": s256}
+    table = {"default": default_scene, "s64": s64, "s256": s256, "default_powers": default_powers,
+             "mixed": synthetic_mixed}
     key = name.lower()
     if key in table:
         return table[key]()

@@ -39,6 +39,22 @@ def exact_eq(a, b) -> bool:
     return type(a) is type(b) and a == b
 
 
+def exact_key(t):
+    """A hashable key with ``exact_key(a) == exact_key(b)`` iff ``exact_eq(a, b)`` (Erlang
+    ``=:=``): numbers keep their int/float type, atoms differ from strings."""
+    if isinstance(t, tuple):
+        return ("T",) + tuple(exact_key(x) for x in t)
+    if isinstance(t, list):
+        return ("L",) + tuple(exact_key(x) for x in t)
+    if isinstance(t, bool):
+        return ("B", t)
+    if isinstance(t, float):
+        return ("F", t)
+    if isinstance(t, int):
+        return ("I", t)
+    return (type(t).__name__, t)
+
+
 # ---- reader ---------------------------------------------------------------------------
 _TOKEN = re.compile(r"""
     (?P<ws>\s+|%[^\n]*)

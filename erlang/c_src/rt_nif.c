@@ -3,18 +3,34 @@
  * MI355X render library (include/rt_mi355x.h, eraytracer_amd/librtmi355x.so).
  *
  * It replaces the pixel loop of raytraced_pixel_list_{simple,concurrent,distributed}/4
- * (raytracer.erl:86-178) with one call into the GPU library:
+ * (raytracer.erl:86-178) with one call into the GPU library, and hands the frame back in
+ * pieces the BEAM can take without one multi-million-element build:
  *
- *   rt_nif:render(Width, Height, Scene, Depth, KeyMode) -> done | [{Key, {R,G,B}}]
- *       KeyMode = simple (every key 1, raytracer.erl:95) | indexed (X+Y*Width, :112, :173)
- *               | distributed (indexed keys, rows shared over every visible GPU, :121-149)
- *   rt_nif:render_binary(Width, Height, Scene, Depth) -> done | binary()   (W*H*3 native doubles)
+ *   rt_nif:render_frame(Width, Height, Scene, Depth, Opts) -> done | Frame
+ *       Opts = #{spp => N, seed => S, devices => all | N}; dirty I/O scheduler.
+ *       Frame = {rt_frame, Width, Height, Rgb, Levels, Lights}: Rgb is W*H*3 native-endian
+ *       doubles, row-major, in pinned host memory (written by DMA; a resource binary);
+ *       Levels is one byte per pixel (reflection-chain levels that hit); Lights is true when
+ *       the scene holds a #point_light{}.
+ *   rt_nif:pixels_chunk(Frame, Start, Count, KeyMode, Tail) -> [{Key, {R,G,B}} | Tail]
+ *       pixels Start .. Start+Count-1 as the reference's list elements, consed onto Tail
+ *       (KeyMode = simple: key 1, raytracer.erl:95 | indexed: X+Y*Width, :112, :173).  A normal
+ *       scheduler call, bounded work: raytracer_gpu builds the whole list from the end in
+ *       chunks, or folds over it chunk by chunk (raytracer_gpu:fold_pixels/4).
+ *   rt_nif:render_binary(Width, Height, Scene, Depth[, Opts]) -> done | binary()
+ *   rt_nif:render_ppm_file(Width, Height, Scene, Depth, Filename) -> ok | done
  *
- * Runs on a dirty I/O scheduler (it blocks while the GPU renders).  The scene list is read
- * record by record (raytracer.erl:72-81) accepting an integer or a float in every numeric
- * slot; exact equality (=:=) between list elements, which shadow_factor/4's match relies on
- * (raytracer.erl:263), is decided here with enif_is_identical and passed down as rt_elem.canon.
- * A malformed scene raises badarg instead of crashing a worker later.
+ * Term types follow the reference exactly: a pixel whose reference value is the integer
+ * triple #colour{r=0,g=0,b=0} — no primary hit (?BACKGROUND_COLOUR, raytracer.erl:82, :201),
+ * depth 0 (pixel_colour_from_ray/3 clause 1, :186-187), or no point light in the scene
+ * (lighting_function/6 folds from #vector{0,0,0}, :250) — is returned as {0,0,0}; every other
+ * pixel as three floats (specular_term's math:pow/2 always yields a float, :289).
+ *
+ * The scene list is read record by record (raytracer.erl:72-81) accepting an integer or a
+ * float in every numeric slot; exact equality (=:=) between list elements, which
+ * shadow_factor/4's match relies on (raytracer.erl:263), is decided here with
+ * enif_is_identical and passed down as rt_elem.canon.  A malformed scene raises badarg
+ * instead of crashing a worker later.
  *
  * Build (needs erl_nif.h, i.e. an Erlang/OTP install; see erlang/Makefile and INTEGRATION.md):
  *   cc -O2 -fPIC -shared -I$ERL_ROOT/usr/include -I../../include rt_nif.c \
@@ -25,7 +41,22 @@
 
 #include "rt_mi355x.h"
 
-static ERL_NIF_TERM atom_done, atom_simple, atom_indexed, atom_distributed, atom_error;
+static ERL_NIF_TERM atom_done, atom_simple, atom_indexed, atom_error, atom_rt_frame, atom_true, atom_false,
+    atom_spp, atom_seed, atom_devices, atom_all, atom_ok, atom_enomem;
+static ErlNifResourceType *pinned_type;
+
+/* a block of pinned host memory (rt_host_alloc) owned by the resource binaries made from it */
+typedef struct {
+    void *p;
+    size_t n;
+} pinned_buf;
+
+static void pinned_dtor(ErlNifEnv *env, void *obj) {
+    (void)env;
+    pinned_buf *b = (pinned_buf *)obj;
+    if (b->p) rt_host_free(b->p);
+    b->p = NULL;
+}
 
 static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
     (void)priv;
@@ -33,8 +64,18 @@ static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
     atom_done = enif_make_atom(env, "done");
     atom_simple = enif_make_atom(env, "simple");
     atom_indexed = enif_make_atom(env, "indexed");
-    atom_distributed = enif_make_atom(env, "distributed");
     atom_error = enif_make_atom(env, "error");
+    atom_rt_frame = enif_make_atom(env, "rt_frame");
+    atom_true = enif_make_atom(env, "true");
+    atom_false = enif_make_atom(env, "false");
+    atom_spp = enif_make_atom(env, "spp");
+    atom_seed = enif_make_atom(env, "seed");
+    atom_devices = enif_make_atom(env, "devices");
+    atom_all = enif_make_atom(env, "all");
+    atom_ok = enif_make_atom(env, "ok");
+    atom_enomem = enif_make_atom(env, "enomem");
+    pinned_type = enif_open_resource_type(env, NULL, "rt_pinned", pinned_dtor, ERL_NIF_RT_CREATE, NULL);
+    if (!pinned_type) return 1;
     return rt_abi_version() == RT_ABI_VERSION ? 0 : 1;
 }
 
@@ -112,17 +153,23 @@ static int marshal_elem(ErlNifEnv *env, ERL_NIF_TERM t, rt_elem *out, int head) 
     return 1;
 }
 
-/* Scene list -> rt_elem array (enif_alloc'd), canon by exact equality.  0 on badarg. */
+/* Scene list -> rt_elem array (enif_alloc'd), canon by exact equality.  0 on badarg; the
+ * arrays are freed by the caller in every case. */
 static int marshal_scene(ErlNifEnv *env, ERL_NIF_TERM list, rt_elem **elems, ERL_NIF_TERM **terms,
-                         unsigned *n_out) {
+                         unsigned *n_out, int *lights) {
     unsigned n, i = 0;
     ERL_NIF_TERM head, tail = list;
+    *elems = NULL;
+    *terms = NULL;
+    *lights = 0;
     if (!enif_get_list_length(env, list, &n) || n == 0) return 0;
     *elems = enif_alloc(n * sizeof(rt_elem));
     *terms = enif_alloc(n * sizeof(ERL_NIF_TERM));
+    if (!*elems || !*terms) return 0;
     while (enif_get_list_cell(env, tail, &head, &tail)) {
         (*terms)[i] = head;
         if (!marshal_elem(env, head, &(*elems)[i], i == 0)) return 0;
+        if ((*elems)[i].kind == RT_POINT_LIGHT) *lights = 1;
         (*elems)[i].canon = (int32_t)i;
         for (unsigned j = 0; j < i; j++) {
             if ((*elems)[j].canon == (int32_t)j && enif_is_identical((*terms)[j], head)) {
@@ -141,109 +188,178 @@ static ERL_NIF_TERM rt_error(ErlNifEnv *env, int rc) {
         env, enif_make_tuple2(env, atom_error, enif_make_string(env, rt_strerror(rc), ERL_NIF_LATIN1)));
 }
 
-/* shared front half: parse args, render into a double buffer */
-static ERL_NIF_TERM render_common(ErlNifEnv *env, const ERL_NIF_TERM argv[], unsigned *W, unsigned *H,
-                                  double **buf, int *done, int all_devices, unsigned spp, ErlNifUInt64 seed) {
+/* W*H*3 doubles in pinned memory as a resource binary (falls back to a plain binary) */
+static int frame_binary(ErlNifEnv *env, size_t bytes, void **data, ERL_NIF_TERM *bin) {
+    pinned_buf *b = enif_alloc_resource(pinned_type, sizeof(pinned_buf));
+    if (!b) return 0;
+    b->n = bytes;
+    b->p = rt_host_alloc(bytes);
+    if (b->p) {
+        *data = b->p;
+        *bin = enif_make_resource_binary(env, b, b->p, bytes);
+        enif_release_resource(b); /* the binary keeps it */
+        return 1;
+    }
+    enif_release_resource(b);
+    ErlNifBinary eb;
+    if (!enif_alloc_binary(bytes, &eb)) return 0;
+    *data = eb.data;
+    *bin = enif_make_binary(env, &eb);
+    return 1;
+}
+
+/* Opts map: spp, seed, devices (all | N) */
+static int get_opts(ErlNifEnv *env, ERL_NIF_TERM m, unsigned *spp, ErlNifUInt64 *seed, int *ndev) {
+    ERL_NIF_TERM v;
+    *spp = 1;
+    *seed = 0;
+    *ndev = 1;
+    if (!enif_is_map(env, m)) return 0;
+    if (enif_get_map_value(env, m, atom_spp, &v) && (!enif_get_uint(env, v, spp) || *spp == 0)) return 0;
+    if (enif_get_map_value(env, m, atom_seed, &v) && !enif_get_uint64(env, v, seed)) return 0;
+    if (enif_get_map_value(env, m, atom_devices, &v)) {
+        if (enif_is_identical(v, atom_all))
+            *ndev = -1;
+        else if (!enif_get_int(env, v, ndev) || *ndev <= 0)
+            return 0;
+    }
+    return 1;
+}
+
+/* Parse (W, H, Scene, Depth), render into *rgb (a new binary) and *lv (levels, optional).
+ * Returns 0 with *ret set (done, badarg or an exception) when there is nothing more to do. */
+static int render_common(ErlNifEnv *env, const ERL_NIF_TERM argv[], unsigned spp, ErlNifUInt64 seed, int ndev,
+                         int want_levels, unsigned *W, unsigned *H, ERL_NIF_TERM *rgb, ERL_NIF_TERM *lv,
+                         int *lights, ERL_NIF_TERM *ret) {
     unsigned D, n = 0;
     rt_elem *elems = NULL;
-    ERL_NIF_TERM *terms = NULL, err = 0;
-    int rc;
-    *done = 0;
-    *buf = NULL;
-    if (!enif_get_uint(env, argv[0], W) || !enif_get_uint(env, argv[1], H) || !enif_get_uint(env, argv[3], &D))
-        return enif_make_badarg(env);
+    ERL_NIF_TERM *terms = NULL;
+    void *data = NULL;
+    ErlNifBinary lvb;
+    int ok = 0, have_lv = 0;
+    if (!enif_get_uint(env, argv[0], W) || !enif_get_uint(env, argv[1], H) || !enif_get_uint(env, argv[3], &D)) {
+        *ret = enif_make_badarg(env);
+        return 0;
+    }
     if (*W == 0 && *H == 0) {
-        *done = 1;
-        return atom_done;
+        *ret = atom_done;
+        return 0;
     }
-    if (*W == 0 || *H == 0) return enif_make_badarg(env); /* function_clause in the reference */
-    if (!marshal_scene(env, argv[2], &elems, &terms, &n)) {
-        err = enif_make_badarg(env);
+    if (*W == 0 || *H == 0) { /* function_clause in the reference */
+        *ret = enif_make_badarg(env);
+        return 0;
+    }
+    if (!marshal_scene(env, argv[2], &elems, &terms, &n, lights)) {
+        *ret = enif_make_badarg(env);
         goto out;
     }
-    *buf = enif_alloc((size_t)*W * *H * 3 * sizeof(double));
-    if (!*buf) {
-        err = enif_raise_exception(env, enif_make_atom(env, "enomem"));
+    if (!frame_binary(env, (size_t)*W * *H * 3 * sizeof(double), &data, rgb)) {
+        *ret = enif_raise_exception(env, atom_enomem);
         goto out;
+    }
+    if (want_levels) {
+        if (!enif_alloc_binary((size_t)*W * *H, &lvb)) {
+            *ret = enif_raise_exception(env, atom_enomem);
+            goto out;
+        }
+        have_lv = 1;
     }
     rt_opts o;
     memset(&o, 0, sizeof o);
     o.struct_size = sizeof o;
-    o.ndev = all_devices ? -1 : 1;
+    o.ndev = ndev;
     o.precision = RT_OUT_F64;
     o.order = RT_ORDER_EXACT;
     o.row_block = 16;
-    o.spp = spp;   /* RT_SUPERSAMPLING (include/rt_mi355x.h); 1 = the reference's pixel */
+    o.out_levels = have_lv ? lvb.data : NULL;
+    o.spp = spp; /* RT_SUPERSAMPLING (include/rt_mi355x.h); 1 = the reference's pixel */
     o.seed = seed;
-    rc = rt_render(elems, n, *W, *H, D, &o, *buf, NULL);
+    int rc = rt_render(elems, n, *W, *H, D, &o, data, NULL);
     if (rc < 0) {
-        enif_free(*buf);
-        *buf = NULL;
-        err = rt_error(env, rc);
+        *ret = rt_error(env, rc);
+        goto out;
     }
+    if (have_lv) {
+        *lv = enif_make_binary(env, &lvb);
+        have_lv = 0;
+    }
+    ok = 1;
 out:
+    if (have_lv) enif_release_binary(&lvb);
     if (elems) enif_free(elems);
     if (terms) enif_free(terms);
-    return err;
+    return ok;
 }
 
-/* render(W, H, Scene, Depth, KeyMode) -> [{Key, {R,G,B}}] in row-major order */
-static ERL_NIF_TERM render_nif(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
-    unsigned W, H;
-    double *buf;
-    int done, keyed, all = 0;
+/* render_frame(W, H, Scene, Depth, Opts) -> done | {rt_frame, W, H, Rgb, Levels, Lights} */
+static ERL_NIF_TERM render_frame_nif(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    unsigned W, H, spp;
+    ErlNifUInt64 seed;
+    int ndev, lights;
+    ERL_NIF_TERM rgb, lv, ret;
     (void)argc;
-    if (enif_is_identical(argv[4], atom_simple)) keyed = 0;
-    else if (enif_is_identical(argv[4], atom_indexed)) keyed = 1;
-    else if (enif_is_identical(argv[4], atom_distributed)) keyed = all = 1;
+    if (!get_opts(env, argv[4], &spp, &seed, &ndev)) return enif_make_badarg(env);
+    if (!render_common(env, argv, spp, seed, ndev, 1, &W, &H, &rgb, &lv, &lights, &ret)) return ret;
+    ERL_NIF_TERM t[6] = {atom_rt_frame, enif_make_uint(env, W), enif_make_uint(env, H), rgb, lv,
+                         lights ? atom_true : atom_false};
+    return enif_make_tuple_from_array(env, t, 6);
+}
+
+/* pixels_chunk(Frame, Start, Count, KeyMode, Tail) -> [{Key, {R,G,B}} | Tail] */
+static ERL_NIF_TERM pixels_chunk_nif(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    const ERL_NIF_TERM *f;
+    int arity, keyed;
+    unsigned W, H;
+    ErlNifUInt64 start, count;
+    ErlNifBinary rgb, lv;
+    (void)argc;
+    if (!enif_get_tuple(env, argv[0], &arity, &f) || arity != 6 || !enif_is_identical(f[0], atom_rt_frame) ||
+        !enif_get_uint(env, f[1], &W) || !enif_get_uint(env, f[2], &H) || !enif_inspect_binary(env, f[3], &rgb) ||
+        !enif_inspect_binary(env, f[4], &lv))
+        return enif_make_badarg(env);
+    const int lights = enif_is_identical(f[5], atom_true);
+    const ErlNifUInt64 npx = (ErlNifUInt64)W * H;
+    if (rgb.size != npx * 3 * sizeof(double) || lv.size != npx) return enif_make_badarg(env);
+    if (!enif_get_uint64(env, argv[1], &start) || !enif_get_uint64(env, argv[2], &count) || start > npx ||
+        count > npx - start)
+        return enif_make_badarg(env);
+    if (enif_is_identical(argv[3], atom_simple)) keyed = 0;
+    else if (enif_is_identical(argv[3], atom_indexed)) keyed = 1;
     else return enif_make_badarg(env);
-    ERL_NIF_TERM r = render_common(env, argv, &W, &H, &buf, &done, all, 1, 0);
-    if (done || !buf) return r;
-    ERL_NIF_TERM list = enif_make_list(env, 0), one = enif_make_int(env, 1);
-    for (size_t i = (size_t)W * H; i-- > 0;) {
-        const double *p = buf + 3 * i;
-        ERL_NIF_TERM rgb = enif_make_tuple3(env, enif_make_double(env, p[0]), enif_make_double(env, p[1]),
-                                            enif_make_double(env, p[2]));
-        ERL_NIF_TERM key = keyed ? enif_make_uint64(env, i) : one;
-        list = enif_make_list_cell(env, enif_make_tuple2(env, key, rgb), list);
+    if (!enif_is_list(env, argv[4])) return enif_make_badarg(env);
+    const double *px = (const double *)rgb.data;
+    ERL_NIF_TERM list = argv[4], one = enif_make_int(env, 1), zero = enif_make_int(env, 0);
+    ERL_NIF_TERM ints = enif_make_tuple3(env, zero, zero, zero);
+    for (ErlNifUInt64 i = start + count; i-- > start;) {
+        ERL_NIF_TERM c;
+        if (!lights || lv.data[i] == 0) {
+            c = ints;
+        } else {
+            const double *p = px + 3 * i;
+            c = enif_make_tuple3(env, enif_make_double(env, p[0]), enif_make_double(env, p[1]),
+                                 enif_make_double(env, p[2]));
+        }
+        list = enif_make_list_cell(env, enif_make_tuple2(env, keyed ? enif_make_uint64(env, i) : one, c), list);
     }
-    enif_free(buf);
     return list;
 }
 
-/* render_binary(W, H, Scene, Depth) -> <<R:64/float-native, G, B, ...>> row-major
- * render_binary(W, H, Scene, Depth, #{spp => N, seed => S}) -> the same, supersampled */
+/* render_binary(W, H, Scene, Depth[, Opts]) -> <<R:64/float-native, G, B, ...>> row-major */
 static ERL_NIF_TERM render_binary_nif(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     unsigned W, H, spp = 1;
     ErlNifUInt64 seed = 0;
-    double *buf;
-    int done;
-    ErlNifBinary bin;
-    if (argc == 5) {
-        ERL_NIF_TERM v;
-        if (!enif_is_map(env, argv[4])) return enif_make_badarg(env);
-        if (enif_get_map_value(env, argv[4], enif_make_atom(env, "spp"), &v) && !enif_get_uint(env, v, &spp))
-            return enif_make_badarg(env);
-        if (enif_get_map_value(env, argv[4], enif_make_atom(env, "seed"), &v) && !enif_get_uint64(env, v, &seed))
-            return enif_make_badarg(env);
-        if (spp == 0) return enif_make_badarg(env);
-    }
-    ERL_NIF_TERM r = render_common(env, argv, &W, &H, &buf, &done, 0, spp, seed);
-    if (done || !buf) return r;
-    size_t nb = (size_t)W * H * 3 * sizeof(double);
-    if (!enif_alloc_binary(nb, &bin)) {
-        enif_free(buf);
-        return enif_raise_exception(env, enif_make_atom(env, "enomem"));
-    }
-    memcpy(bin.data, buf, nb);
-    enif_free(buf);
-    return enif_make_binary(env, &bin);
+    int ndev = 1, lights;
+    ERL_NIF_TERM rgb, lv, ret;
+    if (argc == 5 && !get_opts(env, argv[4], &spp, &seed, &ndev)) return enif_make_badarg(env);
+    if (!render_common(env, argv, spp, seed, ndev, 0, &W, &H, &rgb, &lv, &lights, &ret)) return ret;
+    return rgb;
 }
 
 /* render_ppm_file(W, H, Scene, Depth, Filename) -> ok | done: raytrace/5's render and
  * write_pixels_to_ppm/5 (MaxValue 255) in one call; the P3 text is made on the GPU. */
 static ERL_NIF_TERM render_ppm_file_nif(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     unsigned W, H, D, n = 0;
+    int lights;
     char path[4096];
     rt_elem *elems = NULL;
     ERL_NIF_TERM *terms = NULL, ret;
@@ -253,11 +369,11 @@ static ERL_NIF_TERM render_ppm_file_nif(ErlNifEnv *env, int argc, const ERL_NIF_
     if (enif_get_string(env, argv[4], path, sizeof path, ERL_NIF_LATIN1) <= 0) return enif_make_badarg(env);
     if (W == 0 && H == 0) return atom_done;
     if (W == 0 || H == 0) return enif_make_badarg(env);
-    if (!marshal_scene(env, argv[2], &elems, &terms, &n)) {
+    if (!marshal_scene(env, argv[2], &elems, &terms, &n, &lights)) {
         ret = enif_make_badarg(env);
     } else {
         int rc = rt_render_ppm_file(elems, n, W, H, D, NULL, 255, path, NULL);
-        ret = rc == RT_OK ? enif_make_atom(env, "ok") : rt_error(env, rc);
+        ret = rc == RT_OK ? atom_ok : rt_error(env, rc);
     }
     if (elems) enif_free(elems);
     if (terms) enif_free(terms);
@@ -265,7 +381,8 @@ static ERL_NIF_TERM render_ppm_file_nif(ErlNifEnv *env, int argc, const ERL_NIF_
 }
 
 static ErlNifFunc funcs[] = {
-    {"render", 5, render_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"render_frame", 5, render_frame_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"pixels_chunk", 5, pixels_chunk_nif, 0},
     {"render_binary", 4, render_binary_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"render_binary", 5, render_binary_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"render_ppm_file", 5, render_ppm_file_nif, ERL_NIF_DIRTY_JOB_IO_BOUND},

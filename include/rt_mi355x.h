@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* ---- return codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -110,7 +110,9 @@ typedef struct rt_opts {
     uint8_t *out_levels;  /* optional host W*H bytes: reflection-chain levels that hit, per pixel */
     /* appended in ABI 2 (older callers' smaller struct_size leaves the defaults) */
     uint32_t spp;         /* samples per pixel (default 1 = the reference; see RT_SUPERSAMPLING) */
-    uint32_t reserved0;
+    uint32_t nshards;     /* rt_render: row shards (default 0 = one per device used); shard s runs on
+                             device first_dev + s % ndev, so more shards than devices runs the
+                             distributed strategy's split (raytracer.erl:121-149) on fewer GPUs */
     uint64_t seed;        /* jitter seed for spp > 1 */
 } rt_opts;
 
@@ -132,7 +134,7 @@ typedef struct rt_stats {
     double total_ms;    /* wall time of the whole call, boundary to boundary */
     uint64_t pixels;    /* W*H */
     int32_t ndev;       /* devices actually used */
-    int32_t reserved;
+    int32_t flags;      /* bit 0: out_rgb was pinned host memory (written by DMA directly) */
 } rt_stats;
 
 /* ---- library / device ------------------------------------------------------------ */
@@ -157,9 +159,30 @@ int rt_scene_canon(rt_elem *scene, uint32_t n_elems);
  * Replaces the whole pixel loop (raytracer.erl:86-178): for every pixel (x,y),
  * row-major, out = trace_ray_through_pixel({x/W, y/H}, Scene, Depth).
  * out_rgb: caller-owned host memory, W*H*3 elements of the chosen precision.
- * Returns RT_DONE for W = H = 0, RT_EBADARG if exactly one of them is 0. */
+ * Returns RT_DONE for W = H = 0, RT_EBADARG if exactly one of them is 0.
+ * The process keeps a pool of render contexts per device (streams, device frame buffers, the
+ * wavefront work space, the last scene compiled — recompiled only when the scene's bytes
+ * change), created on first use: the reference calls its strategy once per frame
+ * (raytracer.erl:723-733), and repeated calls pay only the render and the copy.  The frame is
+ * rendered in row bands whose copies to the host overlap the next band's render; memory from
+ * rt_host_alloc (or registered with HIP) is written by DMA directly, other memory through a
+ * pinned staging ring.  Thread-safe: concurrent callers get separate contexts (up to 4 per
+ * device; more wait). */
 int rt_render(const rt_elem *scene, uint32_t n_elems, uint32_t width, uint32_t height,
               uint32_t depth, const rt_opts *opts, void *out_rgb, rt_stats *stats);
+
+/* Pinned (page-locked) host memory for rt_render's out_rgb: the frame is written by DMA
+ * straight into it (a NIF can wrap it in a resource binary; the Python host uses it for its
+ * frames).  rt_host_alloc returns NULL on failure.  Freed blocks are kept for reuse (up to 8
+ * blocks / 4 GiB; a request reuses a block at most twice its size), so allocating one per
+ * frame costs nothing after the first; rt_host_free of a pointer not from rt_host_alloc
+ * returns RT_EBADARG. */
+void *rt_host_alloc(size_t bytes);
+int rt_host_free(void *p);
+/* Free the idle render contexts of the process (device memory, streams) and the cached
+ * pinned blocks; returns the number of contexts still in use by other threads.  The next
+ * rt_render creates them again. */
+int rt_reset_contexts(void);
 
 /* ---- resident-scene API (device buffers, caller's HIP stream) -------------------
  * rt_prepare uploads the scene (and its per-origin constant tables) to one device.
@@ -193,7 +216,17 @@ int rt_release(rt_prepared *p);
  *   their own streams, one context each: the frames then fill each other's latency-bound
  *   tails); -1 = the default (on, unless the environment sets RT_LIT_STREAM=0). */
 #define RT_CFG_SIDE_STREAMS 1
+/* RT_CFG_KERNEL_TIMING: value = a mask of RT_KT_* kernels; every later launch of those kernels
+ *   by this context is bracketed by HIP timing events on the stream it runs on (0 = off, the
+ *   default).  rt_kernel_time reports their summed duration and launch count (it waits for
+ *   the events recorded so far).  Used by bench.py for the roofline of the dominant kernel. */
+#define RT_CFG_KERNEL_TIMING 2
+#define RT_KT_PRIMARY 1  /* k_primary: camera rays and their nearest scan (wavefront engine) */
+#define RT_KT_LEVEL1 2   /* the level-0 shading + level-1 reflection pass (k_reflect_shade(1); with
+                            side streams or levels: k_reflect(1)) */
+#define RT_KT_RENDER 4   /* k_render: the fused engine's one kernel per frame */
 int rt_configure(rt_prepared *p, int option, int64_t value);
+int rt_kernel_time(rt_prepared *p, int kernel, double *total_ms, uint64_t *launches, int reset);
 /* ---- compact slab transfer (the multi-GPU gather; raytracer.erl:151-161 collects pixels) --
  * A slab (as rt_launch writes it) is mostly background pixels, +0.0 in all three channels.
  * For the gather it is sent as a fixed-size header (count of non-zero pixels, u64 at byte

@@ -59,6 +59,19 @@ def _d3(v):
     return (ctypes.c_double * 3)(*[float(x) for x in v])
 
 
+def host_threads() -> int:
+    """Threads for the oracle: this process's CPU share (OMP_NUM_THREADS when set — the GPU box
+    sets it to its 16-CPU share, while os.cpu_count() there reports the whole machine), else
+    the CPUs this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def render(elems, width, height, depth, mode=MEMO, threads=None, row0=0, nrows=None, levels=False, spp=1, seed=0):
     """Render rows [row0, row0+nrows) of a width x height image of the marshalled scene
     `elems`; returns a (nrows, width, 3) float64 array (and the levels array).  spp > 1:
@@ -66,7 +79,7 @@ def render(elems, width, height, depth, mode=MEMO, threads=None, row0=0, nrows=N
     if nrows is None:
         nrows = height - row0
     if threads is None:
-        threads = os.cpu_count() or 1
+        threads = host_threads()
     out = np.zeros((nrows, width, 3), dtype=np.float64)
     lv = np.zeros((nrows, width), dtype=np.uint8) if levels else None
     rc = lib().orc_render_spp(ctypes.cast(elems, ctypes.c_void_p), len(elems), width, height, row0, nrows, depth,

@@ -2,7 +2,7 @@
 """Summarise a scripts/profile.sh run (rocprofv3 kernel trace + separate PMC passes) into one
 JSON (profiles/<name>.json) that DESIGN.md and bench.py cite.
 
-    python scripts/pmc_summary.py gpurun_out/TAG profiles/r01_TAG_pmc.json WORKLOAD_KEY [TIMED_FRAMES]
+    python scripts/pmc_summary.py gpurun_out/TAG profiles/r01_TAG_pmc.json WORKLOAD_KEY [TIMED_FRAMES [ISO_FRAMES]]
 
 The unit is one FRAME LAUNCH (one rt_launch): the dispatch stream is cut into frames at each
 timed frame-start kernel (the wavefront engine's k_primary<PREC, false>, or the fused
@@ -82,7 +82,7 @@ def load_pmc(d):
     return frame, kern, dict(nfr)
 
 
-def load_trace(d, timed=None):
+def load_trace(d, timed=None, iso=0):
     f = glob.glob(os.path.join(d, "trace", "*kernel_trace.csv"))
     if not f:
         return None, None
@@ -106,6 +106,15 @@ def load_trace(d, timed=None):
     # frames in flight overlap: the window from the first frame's first kernel to the last
     # frame's last kernel, per frame, is the GPU time per frame the bench's events measure
     # (over the last `timed` frames: the bench's timed region, after its warmup and a sync)
+    # bench.py ends with `iso` frames launched back to back on one stream (the dominant kernel
+    # timed alone): per-kernel "isolated_avg_ns" over those; the timed frames come before them
+    iso_fr = fr[-iso:] if iso else []
+    if iso:
+        fr = fr[:-iso]
+    iso_k = defaultdict(list)
+    for f in iso_fr:
+        for lab, (s, e, v) in f:
+            iso_k[lab].append(e - s)
     tf = fr[-timed:] if timed else fr
     t_first = min(s for f in tf for _, (s, e, _) in f)
     t_last = max(e for f in tf for _, (s, e, _) in f)
@@ -113,6 +122,8 @@ def load_trace(d, timed=None):
              "avg_span_ns": sum(span) / len(span), "min_busy_ns": min(busy),
              "window_ns_per_frame": (t_last - t_first) / len(tf), "window_frames": len(tf)}
     kern = {lab: {"avg_ns": sum(v) / len(v), "vgpr": vg[lab]} for lab, v in per.items()}
+    for lab, v in iso_k.items():
+        kern.setdefault(lab, {})["isolated_avg_ns"] = sum(v) / len(v)
     return frame, kern
 
 
@@ -145,9 +156,13 @@ def derive(c, ns):
 def main():
     src, dst, key = sys.argv[1], sys.argv[2], sys.argv[3]
     timed = int(sys.argv[4]) if len(sys.argv) > 4 else None  # the bench's --steps
+    spp = int(sys.argv[6]) if len(sys.argv) > 6 else 1       # samples per pixel: spp passes per frame
+    iso = (int(sys.argv[5]) if len(sys.argv) > 5 else 0) * spp  # the bench's --iso (in passes)
+    timed = timed * spp if timed else timed
     pmc, pmc_k, nfr = load_pmc(src)
-    tr, tr_k = load_trace(src, timed)
-    out = {"workload": key, "source": os.path.basename(src.rstrip("/")), "unit": "one frame launch",
+    tr, tr_k = load_trace(src, timed, iso)
+    out = {"workload": key, "source": os.path.basename(src.rstrip("/")),
+           "unit": "one frame launch" if spp == 1 else f"one sample pass ({spp} per frame launch)", "spp": spp,
            "trace": tr, "counters": pmc, "frames_per_counter": nfr,
            # frame-level rates over the GPU time per frame (frames and streams overlap)
            "derived": derive(pmc, tr["window_ns_per_frame"] if tr else None), "kernels": {}}
@@ -166,7 +181,8 @@ def main():
                      indent=1))
     for lab, e in out["kernels"].items():
         x = e["derived"]
-        print(f"{lab:14s} {e.get('avg_ns', 0) / 1e3:8.1f} us vgpr={e.get('vgpr')} "
+        print(f"{lab:14s} {e.get('avg_ns', 0) / 1e3:8.1f} us (alone {e.get('isolated_avg_ns', 0) / 1e3:6.1f}) "
+              f"vgpr={e.get('vgpr')} "
               f"valu/wave={x.get('valu_insts_per_wave', 0):8.0f} f64frac={x.get('f64_issue_frac_of_peak_39.3T', 0):.3f} "
               f"valu_share={x.get('sq_active_inst_valu_share', 0):.3f} lanes={x.get('valu_lane_utilisation', 0):.2f}")
 

@@ -72,12 +72,16 @@ def test_fast_order_and_f32(oracle, name, w, h, d):
 
 
 def test_exact_order_is_bitwise_outside_pow(oracle):
-    """With ORDER_EXACT nearly every pixel is bit-identical to the oracle; report the rest."""
+    """With ORDER_EXACT the frame is bit-identical to the oracle except where the host libm's pow
+    (0.52 ulp, not correctly rounded) differs from the kernels' correctly rounded one: count
+    those pixels and bound them (0.1 %; tests/test_gpu_fullsize.py has the full-size counts)."""
     scene = records.scene()
     img = render(96, 72, scene, 5)
     ref, _ = _oracle(oracle, scene, 96, 72, 5)
-    same = np.all(img.view(np.int64) == ref.view(np.int64), axis=-1)
-    assert same.mean() > 0.9, f"only {same.mean():.3f} of pixels bit-identical"
+    diff = ~np.all(img.view(np.int64) == ref.view(np.int64), axis=-1)
+    print(f"{int(diff.sum())} of {diff.size} pixels not bit-identical")
+    assert diff.sum() <= max(2, diff.size // 1000), f"{int(diff.sum())} pixels not bit-identical"
+    assert np.abs(img - ref).max() <= 1e-15
 
 
 def test_done_and_bad_sizes():

@@ -232,3 +232,45 @@ def test_supersampling_definition(oracle):
                     acc = [acc[i] + c[i] for i in range(3)]
             assert [a / spp for a in acc] == list(img[y, x])
             assert lev0 == lv[y, x]
+
+
+@pytest.mark.parametrize("name,w,h,ds", [("default_powers", 24, 18, (1, 3)), ("mixed", 16, 12, (3,))])
+def test_c_oracle_equals_term_restatement_edge_scenes(oracle, name, w, h, ds):
+    """Specular powers 0 (math:pow(0, 0) = 1.0), 0.5, 2.5 and 1025 (the general math:pow/2
+    path, :289), and a scene with triangles (one back-facing) and two planes among 48 spheres:
+    the C oracle equals the term-level restatement bit for bit."""
+    scene = scenes.named(name)
+    el = N.marshal(scene)
+    for d in ds:
+        a = oracle.render(el, w, h, d, mode=oracle.MEMO)
+        b = _py(scene, w, h, d)
+        assert np.array_equal(_bits(a), _bits(b)), f"{name} depth {d}"
+
+
+def _int_zero_rule(scene, levels):
+    """Where the reference returns integer channels: no hit at the primary ray (?BACKGROUND_COLOUR,
+    :82, :201), depth 0 (pixel_colour_from_ray/3 clause 1, :186-187; levels are 0 there too), or
+    no point light in the scene (lighting_function/6 folds from #vector{0,0,0}, :250).  Every
+    other pixel is all floats: specular_term's math:pow/2 (:289) always returns a float."""
+    no_lights = not any(t[0] == "point_light" for t in scene)
+    return (levels == 0) | no_lights
+
+
+@pytest.mark.parametrize("mk,d", [(lambda: R.scene(), 3), (lambda: R.scene(), 0), (lambda: TRICKY[2](), 3),
+                                  (lambda: scenes.default_powers(), 2), (lambda: TRICKY[3](), 1)])
+def test_term_types_rule(oracle, mk, d):
+    """The exact term types of the reference's pixel list (int 0 vs float 0.0 are not =:=)
+    follow _int_zero_rule, which the NIF (erlang/c_src/rt_nif.c) and the Python host
+    (raytracer._pixel_list) apply from the per-pixel levels: checked against the term-level
+    restatement, which keeps Erlang's int/float types."""
+    scene = mk()
+    w, h = 20, 15
+    px = E.raytraced_pixel_list_simple(w, h, scene, d)
+    _, lv = oracle.render(N.marshal(scene), w, h, d, mode=oracle.MEMO, levels=True)
+    rule = _int_zero_rule(scene, lv).ravel()
+    for i, (_key, rgb) in enumerate(px):
+        kinds = {type(c) for c in rgb}
+        if rule[i]:
+            assert kinds == {int} and rgb == (0, 0, 0), (i, rgb)
+        else:
+            assert kinds == {float}, (i, rgb)
