@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=1, help="samples per pixel (RT_SUPERSAMPLING; BASELINE config 5: 16)")
     ap.add_argument("--seed", type=int, default=0x5EED0005)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
+    ap.add_argument("--settle", type=float, default=0.3,
+                    help="seconds of untimed frames before the warmup steps (clock ramp; 0 = none)")
     ap.add_argument("--iso", type=int, default=20,
                     help="frames launched back to back after the timed region to time the dominant kernel alone")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -230,6 +232,16 @@ def main():
         else:
             pipe.submit()
 
+    # Before the W warmup steps: render frames until --settle seconds have passed (the GPU's
+    # clocks ramp over the first ~50 frames; with a short --warmup the timed steps would still
+    # see them rising).  Frames only, no gather.
+    settle_frames = 0
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < args.settle:
+        for _ in range(8):
+            fr.launch()
+        settle_frames += 8
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         one_step()
     if pipe is not None:
@@ -345,6 +357,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_frames": settle_frames,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
             "scaling": "strong",
