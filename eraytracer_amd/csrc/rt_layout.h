@@ -42,6 +42,8 @@ constexpr double CULL_EPS = 1.0e-9; // angular / relative safety margin of the c
 // int-table record widths (ints)
 constexpr int OBJ_META_W = 4; // kind, local index within its type, canon compact id, canon's local index
 
+constexpr int LDS_STAGE_MAX = 32 * 1024; // 5 workgroups per CU keep their 32 KiB each
+
 enum ObjKind : int { K_SPHERE = 0, K_TRIANGLE = 1, K_PLANE = 2 };
 
 // Scalar header passed to the kernel by value.  All offsets index the double table `tab`
@@ -58,6 +60,11 @@ struct SceneHdr {
     // the uint64 at itab[i_occ + 2*((i*n_sph + t)*n_chunk + k)] has bit j set iff sphere
     // 64k+j can block a shadow ray from light i to any point of sphere t (see rt_scene.cpp).
     int i_occ, n_chunk;
+    // LDS staging (spheres-only scenes with culling whose per-lane-gathered tables fit
+    // LDS_STAGE_MAX bytes; l_bytes = 0 otherwise): byte offsets in the workgroup's dynamic LDS of
+    // the object rows (o_obj), object meta rows (i_obj_meta), the lights' per-origin sphere rows
+    // (o_sph_org from origin 1 on), the occluder masks (i_occ) and the sphere ids (i_sph_id).
+    int l_obj, l_meta, l_org, l_occ, l_id, l_bytes;
     // camera (point_on_screen/3, :486-503, with focal_length/2 :483-484 folded in)
     double cam_x, cam_y, cam_z; // Camera#camera.location
     double sx;   // 0*F + Lx            (first fold step, x)

@@ -232,6 +232,63 @@ struct Scene {
     const int *__restrict__ itab;
 };
 
+// ---- scene table access; SPH (template argument of the shading code): 0 = any scene, 1 = spheres
+// only (occluder masks), 2 = spheres only with the per-lane-gathered tables staged in LDS.
+// Lanes of a wave read these rows by their own object / target / candidate (gathers whose L2
+// round trips the shading waits on); staged, they are LDS reads.  Wave-uniform reads stay
+// scalar loads from the tables in HBM (scalar cache).
+extern __shared__ __attribute__((aligned(16))) char g_lds[];
+
+template <int SPH>
+__device__ __forceinline__ const double *obj_row(const Scene &S, int id) {
+    if (SPH == 2) return reinterpret_cast<const double *>(g_lds + S.h.l_obj) + id * OBJ_W;
+    return S.tab + S.h.o_obj + id * OBJ_W;
+}
+template <int SPH>
+__device__ __forceinline__ int4 obj_meta(const Scene &S, int id) {
+    if (SPH == 2) return reinterpret_cast<const int4 *>(g_lds + S.h.l_meta)[id];
+    return *reinterpret_cast<const int4 *>(S.itab + S.h.i_obj_meta + id * OBJ_META_W);
+}
+// per-origin sphere row (o - c, C); staged only for the light origins (org >= 1)
+template <int SPH>
+__device__ __forceinline__ const double *org_row(const Scene &S, int org, int k) {
+    if (SPH == 2) return reinterpret_cast<const double *>(g_lds + S.h.l_org) + ((org - 1) * S.h.n_sph + k) * SPH_ORG_W;
+    return S.tab + S.h.o_sph_org + (org * S.h.n_sph + k) * SPH_ORG_W;
+}
+// occluder masks of `light`, chunk `chunk64`: element t*n_chunk is target sphere t's mask
+template <int SPH>
+__device__ __forceinline__ const unsigned long long *occ_masks(const Scene &S, int light, int chunk64) {
+    const int w = (light * S.h.n_sph) * S.h.n_chunk + chunk64;
+    if (SPH == 2) return reinterpret_cast<const unsigned long long *>(g_lds + S.h.l_occ) + w;
+    return reinterpret_cast<const unsigned long long *>(S.itab + S.h.i_occ) + w;
+}
+template <int SPH>
+__device__ __forceinline__ int sph_id(const Scene &S, int k) {
+    if (SPH == 2) return reinterpret_cast<const int *>(g_lds + S.h.l_id)[k];
+    return S.itab[S.h.i_sph_id + k];
+}
+// Copy the staged tables into this workgroup's LDS (every thread of the block, before any use).
+template <int SPH>
+__device__ __forceinline__ void stage_tables(const Scene &S) {
+    if (SPH != 2) return;
+    const SceneHdr &h = S.h;
+    auto copy16 = [&](int dst, const void *src, int bytes) { // src 16-byte aligned
+        const int4 *s4 = reinterpret_cast<const int4 *>(src);
+        int4 *d4 = reinterpret_cast<int4 *>(g_lds + dst);
+        for (int i = threadIdx.x; i < bytes / 16; i += blockDim.x) d4[i] = s4[i];
+    };
+    auto copy4 = [&](int dst, const int *src, int n) {
+        int *d = reinterpret_cast<int *>(g_lds + dst);
+        for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = src[i];
+    };
+    copy16(h.l_obj, S.tab + h.o_obj, h.n_obj * OBJ_W * 8);
+    copy16(h.l_meta, S.itab + h.i_obj_meta, h.n_obj * OBJ_META_W * 4);
+    copy16(h.l_org, S.tab + h.o_sph_org + h.n_sph * SPH_ORG_W, h.n_light * h.n_sph * SPH_ORG_W * 8);
+    copy4(h.l_occ, S.itab + h.i_occ, h.n_light * h.n_sph * h.n_chunk * 2); // 8-byte aligned in the int table
+    copy4(h.l_id, S.itab + h.i_sph_id, h.n_sph);
+    __syncthreads();
+}
+
 // Diagnostic build only (-DRT_STATS): per-wave event counters read back with rt_debug_stats().
 #ifdef RT_STATS
 __device__ unsigned long long g_stats[16];
@@ -697,9 +754,10 @@ __device__ __forceinline__ Beam shadow_cone(const HitBall &hb, const D3 &Lp, dou
 struct Target {
     int c, kind, loc, skip;
 };
+template <int SPH = 0>
 __device__ __forceinline__ Target make_target(const Scene &S, int obj, bool active) {
     // one row: kind, local, canonical id, the canonical element's local index (same kind)
-    const int4 mt = *reinterpret_cast<const int4 *>(S.itab + S.h.i_obj_meta + obj * OBJ_META_W);
+    const int4 mt = obj_meta<SPH>(S, obj);
     Target T;
     T.c = mt.z;
     T.kind = mt.x;
@@ -717,7 +775,7 @@ __device__ __forceinline__ Target make_target(const Scene &S, int obj, bool acti
 
 // SPH: the scene holds only spheres and culling is on (host-checked), so every target is a
 // sphere with occluder masks: the cone and triangle/plane paths are compiled out (registers).
-template <bool SPH = false>
+template <int SPH = 0>
 __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &T, const D3 &sd, bool active,
                                        const HitBall &hb, const D3 &Lp) {
     const SceneHdr &h = S.h;
@@ -729,7 +787,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
     bool valid = false;
     if (active) {
         if (SPH || kind == K_SPHERE) {
-            const double *q = S.tab + h.o_sph_org + (org * h.n_sph + loc) * SPH_ORG_W;
+            const double *q = org_row<SPH>(S, org, loc);
             double B = 2 * (sd.x * q[0] + sd.y * q[1] + sd.z * q[2]);
             valid = sph_t(B, q[3], A4, ts);
         } else if (kind == K_TRIANGLE) {
@@ -760,8 +818,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
             // Every lane walks its own target's occluder mask: the trip count is the largest
             // per-lane candidate count, not the size of the union over the wave's targets
             // (which grows with every distinct target an incoherent wave holds).
-            const unsigned long long *occ = reinterpret_cast<const unsigned long long *>(
-                S.itab + h.i_occ + 2 * ((light * h.n_sph) * h.n_chunk + (chunk >> 6)));
+            const unsigned long long *occ = occ_masks<SPH>(S, light, chunk >> 6);
             unsigned long long mine = blocked ? 0ull : occ[loc * h.n_chunk]; // never holds the target
             for (;;) {
                 const bool w = !blocked && mine != 0;
@@ -769,9 +826,9 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
                 const int k = chunk + (w ? __builtin_ctzll(mine) : 0);
                 mine &= mine - 1;
                 RT_STAT(ST_SHADOW_ITER, 1);
-                const double2 *q = reinterpret_cast<const double2 *>(S.tab + h.o_sph_org + (org * h.n_sph + k) * SPH_ORG_W);
+                const double2 *q = reinterpret_cast<const double2 *>(org_row<SPH>(S, org, k));
                 const double2 q01 = q[0], q23 = q[1];
-                const int id = S.itab[h.i_sph_id + k];
+                const int id = sph_id<SPH>(S, k);
                 const double B = 2 * (sd.x * q01.x + sd.y * q01.y + sd.z * q23.x);
                 double t;
                 const bool hit = sph_t_wave(B, q23.y, A4, t);
@@ -831,13 +888,13 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
 // re-read per light for the same reason.
 // bits (optional): bit i set where light i's shadow test passed (lights 0..31; only lanes whose
 // light term is not exactly zero are tested, the others' bits are 0 and never matter).
-template <bool GENPOW, bool SPH = false>
+template <bool GENPOW, int SPH = 0>
 __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D3 &hit, const D3 &N, const D3 &col,
                                     double refl, bool active, unsigned *bits = nullptr) {
     const SceneHdr &h = S.h;
     if (__ballot(active) == 0) return D3{0.0, 0.0, 0.0}; // no hit to shade in this wave
-    const double *m = S.tab + h.o_obj + id * OBJ_W;
-    const Target T = make_target(S, id, active);
+    const double *m = obj_row<SPH>(S, id);
+    const Target T = make_target<SPH>(S, id, active);
     // the hit ball is only needed for non-sphere shadow targets (see lit_by)
     HitBall hb;
     hb.on = false;
@@ -1447,8 +1504,16 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     HitRec *q = static_cast<HitRec *>(p->d_queue);
     const int nrefl = (p->hdr.n_light > 0 && D > 1) ? D - 1 : 0;
     const int nshade = D > 0 ? 1 + nrefl : 0;
-    // spheres only, culling on: every shadow target has occluder masks (lit_by<true>)
+    // spheres only, culling on: every shadow target has occluder masks (lit_by<1>); their
+    // per-lane-gathered tables staged in each workgroup's LDS when they fit (SPH = 2;
+    // RT_LDS_STAGE=0 keeps them in HBM, for A/B runs)
     const bool sph_only = p->hdr.n_tri == 0 && p->hdr.n_pl == 0 && p->hdr.cull_ok;
+    static const bool stage_env = [] {
+        const char *e = std::getenv("RT_LDS_STAGE");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    const bool staged = sph_only && stage_env && p->hdr.l_bytes > 0;
+    const size_t lds = staged ? (size_t)p->hdr.l_bytes : 0;
     // no side streams (frames in flight): each level's shading fused into the next reflection
     // pass (k_reflect_shade); RT_FUSE_SHADE=0 keeps separate k_light launches, for A/B runs
     static const bool fuse_env = [] {
@@ -1498,11 +1563,14 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             // levels >= 2 are shaded here only when dense (decided on the device; otherwise the
             // launch exits at once): a smaller persistent grid keeps the empty launch cheap
             const int lblocks = k >= 2 ? std::min(sblocks, DEEP_LIGHT_BLOCKS) : sblocks;
-            if (sph_only)
-                hipLaunchKernelGGL((k_light<PREC, GENPOW, true>), dim3(lblocks), dim3(BLOCK), 0, ls(k), p->hdr,
+            if (staged)
+                hipLaunchKernelGGL((k_light<PREC, GENPOW, 2>), dim3(lblocks), dim3(BLOCK), lds, ls(k), p->hdr,
+                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k));
+            else if (sph_only)
+                hipLaunchKernelGGL((k_light<PREC, GENPOW, 1>), dim3(lblocks), dim3(BLOCK), 0, ls(k), p->hdr,
                                    p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k));
             else
-                hipLaunchKernelGGL((k_light<PREC, GENPOW, false>), dim3(lblocks), dim3(BLOCK), 0, ls(k), p->hdr,
+                hipLaunchKernelGGL((k_light<PREC, GENPOW, 0>), dim3(lblocks), dim3(BLOCK), 0, ls(k), p->hdr,
                                    p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k));
             HIPCHK(hipGetLastError());
             if (overlap) HIPCHK(hipEventRecord(p->ev_lit[k], ls(k)));
@@ -1514,14 +1582,16 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             // waves each, bound by one wave's dependent chain: they walk two candidates per step
             KtScope kt(p, k == 1 ? RT_KT_LEVEL1 : 0, st);
             if (fuse) {
-#define RT_RS(SPHV, ILPV)                                                                                           \
-    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab, \
-                       p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1), colk(k - 1), \
-                       litk(k - 1))
-                if (sph_only && k == 1) RT_RS(true, false);
-                else if (sph_only) RT_RS(true, true);
-                else if (k == 1) RT_RS(false, false);
-                else RT_RS(false, true);
+#define RT_RS(SPHV, ILPV, LDSV)                                                                                     \
+    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV>), dim3(sblocks), dim3(BLOCK), LDSV, st, p->hdr,        \
+                       p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
+                       colk(k - 1), litk(k - 1))
+                if (staged && k == 1) RT_RS(2, false, lds);
+                else if (staged) RT_RS(2, true, lds);
+                else if (sph_only && k == 1) RT_RS(1, false, 0);
+                else if (sph_only) RT_RS(1, true, 0);
+                else if (k == 1) RT_RS(0, false, 0);
+                else RT_RS(0, true, 0);
 #undef RT_RS
             } else if (lv && k == 1)
                 hipLaunchKernelGGL((k_reflect<true, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
@@ -1546,13 +1616,15 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             const size_t ls_ = (size_t)ntiles * TILE_SLOTS;
             const bool bits = p->hdr.n_light <= 32; // the shadow answers fit the record
             auto walk = [&](hipStream_t s_, int lo, int hi) {
-#define RT_WALK(SPHV, BITSV)                                                                                        \
-    hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV>), dim3(sblocks), dim3(BLOCK), 0, s_, p->hdr, p->d_tab,    \
+#define RT_WALK(SPHV, BITSV, LDSV)                                                                                  \
+    hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV>), dim3(sblocks), dim3(BLOCK), LDSV, s_, p->hdr, p->d_tab, \
                        p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child, p->d_lit, lo, hi)
-                if (sph_only && bits) RT_WALK(true, true);
-                else if (sph_only) RT_WALK(true, false);
-                else if (bits) RT_WALK(false, true);
-                else RT_WALK(false, false);
+                if (staged && bits) RT_WALK(2, true, lds);
+                else if (staged) RT_WALK(2, false, lds);
+                else if (sph_only && bits) RT_WALK(1, true, 0);
+                else if (sph_only) RT_WALK(1, false, 0);
+                else if (bits) RT_WALK(0, true, 0);
+                else RT_WALK(0, false, 0);
 #undef RT_WALK
             };
             if (overlap) { // side stream 0 (after level 0's shading) waits for level 1's, and for
@@ -1564,11 +1636,14 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                 HIPCHK(hipEventRecord(p->ev_lit[0], p->side[0]));
             }
             if (D > 2) {
-                if (sph_only)
-                    hipLaunchKernelGGL((k_walk_deep<GENPOW, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
+                if (staged)
+                    hipLaunchKernelGGL((k_walk_deep<GENPOW, 2>), dim3(sblocks), dim3(BLOCK), lds, st, p->hdr,
+                                       p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, colk(2));
+                else if (sph_only)
+                    hipLaunchKernelGGL((k_walk_deep<GENPOW, 1>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
                                        p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, colk(2));
                 else
-                    hipLaunchKernelGGL((k_walk_deep<GENPOW, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
+                    hipLaunchKernelGGL((k_walk_deep<GENPOW, 0>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
                                        p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, colk(2));
                 HIPCHK(hipGetLastError());
             }
