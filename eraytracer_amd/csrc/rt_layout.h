@@ -63,8 +63,9 @@ struct SceneHdr {
     // LDS staging (spheres-only scenes with culling whose per-lane-gathered tables fit
     // LDS_STAGE_MAX bytes; l_bytes = 0 otherwise): byte offsets in the workgroup's dynamic LDS of
     // the object rows (o_obj), object meta rows (i_obj_meta), the lights' per-origin sphere rows
-    // (o_sph_org from origin 1 on), the occluder masks (i_occ) and the sphere ids (i_sph_id).
-    int l_obj, l_meta, l_org, l_occ, l_id, l_bytes;
+    // (o_sph_org from origin 1 on), the occluder masks (i_occ), the sphere ids (i_sph_id) and
+    // the sphere bounds of the reflection rays' beam culling (o_sph_b).
+    int l_obj, l_meta, l_org, l_occ, l_id, l_sphb, l_bytes;
     // camera (point_on_screen/3, :486-503, with focal_length/2 :483-484 folded in)
     double cam_x, cam_y, cam_z; // Camera#camera.location
     double sx;   // 0*F + Lx            (first fold step, x)

@@ -286,6 +286,7 @@ __device__ __forceinline__ void stage_tables(const Scene &S) {
     copy16(h.l_org, S.tab + h.o_sph_org + h.n_sph * SPH_ORG_W, h.n_light * h.n_sph * SPH_ORG_W * 8);
     copy4(h.l_occ, S.itab + h.i_occ, h.n_light * h.n_sph * h.n_chunk * 2); // 8-byte aligned in the int table
     copy4(h.l_id, S.itab + h.i_sph_id, h.n_sph);
+    copy16(h.l_sphb, S.tab + h.o_sph_b, h.n_sph * SPH_B_W * 8);
     __syncthreads();
 }
 
@@ -415,6 +416,7 @@ __device__ __forceinline__ Beam make_beam(const SceneHdr &h, bool act, const D3 
 // org >= 0: the beam starts at tabled origin `org` (camera / light) and uses its cone table;
 // a sphere whose nearest surface point is farther than tmax from the origin is dropped too
 // (its hits have t > tmax; shadow scans only care about t <= t*, and t* <= tmax).
+template <int SPH = 0>
 __device__ __forceinline__ unsigned long long cull_chunk(const Scene &S, const Beam &b, int chunk, int org,
                                                          double tmax = __builtin_inf()) {
     // Branch-free: every load of the record is issued at once and the decision is a mask.
@@ -430,7 +432,8 @@ __device__ __forceinline__ unsigned long long cull_chunk(const Scene &S, const B
         const double av = b.ax * q01.x + b.ay * q01.y + b.az * q23.x;  // |v| cos(phi)
         keep = ((q67.x != 0.0) | !(av + CULL_EPS * q23.y < thr * q23.y)) & !(q67.y > tmax);
     } else {
-        const double2 *g = reinterpret_cast<const double2 *>(S.tab + h.o_sph_b + kk * SPH_B_W);
+        const double2 *g = SPH == 2 ? reinterpret_cast<const double2 *>(g_lds + h.l_sphb) + kk * (SPH_B_W / 2)
+                                    : reinterpret_cast<const double2 *>(S.tab + h.o_sph_b + kk * SPH_B_W);
         const double2 g01 = g[0], g23 = g[1];
         const double vx = g01.x - b.mx, vy = g01.y - b.my, vz = g23.x - b.mz;
         const double vl = sqrt(vx * vx + vy * vy + vz * vz);
@@ -548,7 +551,7 @@ __device__ __forceinline__ void scan_tri_pl(const Scene &S, int org, const D3 &o
 }
 
 constexpr int MAX_GROUPS = 3;
-template <bool PRE, bool ILP = false>
+template <bool PRE, bool ILP = false, int SPH = 0>
 __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, bool act,
                                        int grp = -1) {
     const SceneHdr &h = S.h;
@@ -574,7 +577,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
                 all = true;
                 break;
             }
-            m |= cull_chunk(S, b, 0, -1);
+            m |= cull_chunk<SPH>(S, b, 0, -1);
         }
         if (all) m = chunk_all(h.n_sph, 0);
         scan_spheres<false, ILP>(S, org, o, d, A4, 0, m, bt, bid);
@@ -591,7 +594,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
         RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
         for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
             const unsigned long long m =
-                b.on ? cull_chunk(S, b, chunk, PRE ? org : -1) : chunk_all(h.n_sph, chunk);
+                b.on ? cull_chunk<SPH>(S, b, chunk, PRE ? org : -1) : chunk_all(h.n_sph, chunk);
             scan_spheres<PRE, ILP>(S, org, o, d, A4, chunk, m, bt, bid);
         }
         if (!b.on) break; // everything was scanned
@@ -1560,6 +1563,10 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                 HIPCHK(hipStreamWaitEvent(ls(k), p->ev_level[k], 0));
             }
             if (fuse && k < nrefl) return RT_OK; // shaded by k_reflect_shade(k + 1)
+            if (k == nrefl && k >= 2) { // the deepest level >= 2: shaded by k_walk_deep / k_walk
+                if (overlap) HIPCHK(hipEventRecord(p->ev_lit[k], ls(k)));
+                return RT_OK;
+            }
             // levels >= 2 are shaded here only when dense (decided on the device; otherwise the
             // launch exits at once): a smaller persistent grid keeps the empty launch cheap
             const int lblocks = k >= 2 ? std::min(sblocks, DEEP_LIGHT_BLOCKS) : sblocks;
@@ -1650,10 +1657,10 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             if (overlap) {
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[nrefl], 0));
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
+                if (D > 2) walk(st, 2, D);
             } else {
-                walk(st, 1, 2);
+                walk(st, 1, D); // every chain in one launch (levels 2.. after k_walk_deep)
             }
-            if (D > 2) walk(st, 2, D);
             HIPCHK(hipGetLastError());
         } else if (overlap && nshade > 0) {
             HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));

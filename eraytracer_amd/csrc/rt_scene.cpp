@@ -351,7 +351,7 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
     h.screen_h = SH;
     h.n_light_d = (double)h.n_light;
     // LDS staging layout (16-byte aligned sections)
-    h.l_obj = h.l_meta = h.l_org = h.l_occ = h.l_id = -1;
+    h.l_obj = h.l_meta = h.l_org = h.l_occ = h.l_id = h.l_sphb = -1;
     h.l_bytes = 0;
     if (h.cull_ok && h.n_tri == 0 && h.n_pl == 0 && h.n_sph > 0 && h.n_light > 0) {
         auto up16 = [](long v) { return (v + 15) / 16 * 16; };
@@ -361,9 +361,10 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
         const long l_org = off; off = up16(off + (long)h.n_light * h.n_sph * SPH_ORG_W * 8);
         const long l_occ = off; off = up16(off + (long)h.n_light * h.n_sph * h.n_chunk * 8);
         const long l_id = off; off = up16(off + (long)h.n_sph * 4);
+        const long l_sphb = off; off = up16(off + (long)h.n_sph * SPH_B_W * 8);
         if (off <= LDS_STAGE_MAX) {
             h.l_obj = (int)l_obj; h.l_meta = (int)l_meta; h.l_org = (int)l_org; h.l_occ = (int)l_occ;
-            h.l_id = (int)l_id; h.l_bytes = (int)off;
+            h.l_id = (int)l_id; h.l_sphb = (int)l_sphb; h.l_bytes = (int)off;
         }
     }
     return RT_OK;
