@@ -1541,6 +1541,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         auto litk = [&](int k) { return p->d_lit + (size_t)k * ntiles * TILE_SLOTS; };
         HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
+        const PassGeom g{W, H, rb, sh, ns, row0, spp, sample, seed}; // level-0 records are rebuilt from it
         dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
         {
             KtScope kt(p, RT_KT_PRIMARY, st);
@@ -1572,13 +1573,13 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             const int lblocks = k >= 2 ? std::min(sblocks, DEEP_LIGHT_BLOCKS) : sblocks;
             if (staged)
                 hipLaunchKernelGGL((k_light<PREC, GENPOW, 2>), dim3(lblocks), dim3(BLOCK), lds, ls(k), p->hdr,
-                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k));
+                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k), g);
             else if (sph_only)
                 hipLaunchKernelGGL((k_light<PREC, GENPOW, 1>), dim3(lblocks), dim3(BLOCK), 0, ls(k), p->hdr,
-                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k));
+                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k), g);
             else
                 hipLaunchKernelGGL((k_light<PREC, GENPOW, 0>), dim3(lblocks), dim3(BLOCK), 0, ls(k), p->hdr,
-                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k));
+                                   p->d_tab, p->d_itab, k, o, qk(k), ik(k), nitems + k, colk(k), litk(k), g);
             HIPCHK(hipGetLastError());
             if (overlap) HIPCHK(hipEventRecord(p->ev_lit[k], ls(k)));
             return RT_OK;
@@ -1592,7 +1593,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
 #define RT_RS(SPHV, ILPV, LDSV)                                                                                     \
     hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV>), dim3(sblocks), dim3(BLOCK), LDSV, st, p->hdr,        \
                        p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
-                       colk(k - 1), litk(k - 1))
+                       colk(k - 1), litk(k - 1), g)
                 if (staged && k == 1) RT_RS(2, false, lds);
                 else if (staged) RT_RS(2, true, lds);
                 else if (sph_only && k == 1) RT_RS(1, false, 0);
@@ -1602,16 +1603,16 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
 #undef RT_RS
             } else if (lv && k == 1)
                 hipLaunchKernelGGL((k_reflect<true, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1));
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             else if (lv)
                 hipLaunchKernelGGL((k_reflect<true, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1));
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             else if (k == 1)
                 hipLaunchKernelGGL((k_reflect<false, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1));
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             else
                 hipLaunchKernelGGL((k_reflect<false, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
-                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1));
+                                   p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             HIPCHK(hipGetLastError());
             if ((rc = level_lists(k)) != RT_OK) return rc;
         }
@@ -1625,7 +1626,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             auto walk = [&](hipStream_t s_, int lo, int hi) {
 #define RT_WALK(SPHV, BITSV, LDSV)                                                                                  \
     hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV>), dim3(sblocks), dim3(BLOCK), LDSV, s_, p->hdr, p->d_tab, \
-                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child, p->d_lit, lo, hi)
+                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child, p->d_lit, lo, hi, g)
                 if (staged && bits) RT_WALK(2, true, lds);
                 else if (staged) RT_WALK(2, false, lds);
                 else if (sph_only && bits) RT_WALK(1, true, 0);
