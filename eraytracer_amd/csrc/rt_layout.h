@@ -38,6 +38,7 @@ constexpr int SPH_OB_W = 8;  // vx vy vz (= c - o), |v|, sin(rho) upper bound, c
 // far below its 0.001 discriminant threshold: all scene coordinates within this bound.
 constexpr double CULL_EXTENT = 1.0e4;
 constexpr double CULL_EPS = 1.0e-9; // angular / relative safety margin of the cull tests
+constexpr int BEAM_MIN_SPHERES = 8;  // fewer spheres: scans test every sphere (no wave beams)
 
 // int-table record widths (ints)
 constexpr int OBJ_META_W = 4; // kind, local index within its type, canon compact id, canon's local index
@@ -50,7 +51,8 @@ enum ObjKind : int { K_SPHERE = 0, K_TRIANGLE = 1, K_PLANE = 2 };
 // or the int table `itab` (both device allocations owned by an rt_prepared).
 struct SceneHdr {
     int n_sph, n_tri, n_pl, n_obj, n_light, n_org; // n_org = 1 + n_light
-    int cull_ok;                                   // scene within CULL_EXTENT: beam culling allowed
+    int cull_ok;                                   // scene within CULL_EXTENT: culling allowed (occluder masks)
+    int beam_ok;                                   // cull_ok and enough spheres that wave beams pay
     int int_pow;                                   // every specular power is an integer in [0, 1024]
     // offsets into tab
     int o_sph, o_sph_org, o_tri, o_tri_org, o_pl, o_pl_org, o_obj, o_light, o_sph_b, o_sph_ob;

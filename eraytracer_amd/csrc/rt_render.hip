@@ -374,7 +374,7 @@ __device__ __forceinline__ Beam make_beam(const SceneHdr &h, bool act, const D3 
     b.on = false;
     b.ax = b.ay = b.az = b.c = b.s = b.mx = b.my = b.mz = b.ro = 0.0;
     const unsigned long long am = __ballot(act);
-    if (!h.cull_ok || am == 0) return b;
+    if (!h.beam_ok || am == 0) return b;
     // Axis: the (normalised) direction of one active lane — the tile centre when it is active.
     // Any axis inside the bundle gives a valid cone, at most twice as wide as the best one.
     const int al = ((am >> 27) & 1) ? 27 : __builtin_ctzll(am);
@@ -610,7 +610,7 @@ __device__ __forceinline__ Beam make_beam_pair(const SceneHdr &h, bool a0, const
     b.on = false;
     b.ax = b.ay = b.az = b.c = b.s = b.mx = b.my = b.mz = b.ro = 0.0;
     const unsigned long long m0 = __ballot(a0), m1 = __ballot(a1);
-    if (!h.cull_ok || (m0 | m1) == 0) return b;
+    if (!h.beam_ok || (m0 | m1) == 0) return b;
     // axis: the ray of pixel (3, 7) of the block (set 0, lane 59), else the first active ray
     double rx, ry, rz;
     if ((m0 >> 59) & 1) {
@@ -713,7 +713,7 @@ __device__ __forceinline__ HitBall make_hitball(const SceneHdr &h, bool act, con
     hb.on = false;
     hb.cx = hb.cy = hb.cz = hb.r = 0.0;
     const unsigned long long am = __ballot(act);
-    if (!h.cull_ok || am == 0) return hb;
+    if (!h.beam_ok || am == 0) return hb;
     const double inv_n = 1.0 / (double)__popcll(am);
     hb.cx = uniform(wave_sum(act ? hit.x : 0.0) * inv_n);
     hb.cy = uniform(wave_sum(act ? hit.y : 0.0) * inv_n);

@@ -5,6 +5,7 @@
 // binary64, compiled with -ffp-contract=off, so the kernel sees bit-identical values to
 // those the reference computes per ray.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -255,6 +256,16 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
             grow(s.center.x); grow(s.center.y); grow(s.center.z); grow(s.radius);
         }
         h.cull_ok = ext <= CULL_EXTENT ? 1 : 0;
+    }
+    // Wave beams (a cone over the wave's rays, a candidate mask per 64 spheres) cost a few wave
+    // reductions per scan; with a handful of spheres testing every one is cheaper
+    // (RT_BEAM_MIN overrides the threshold, for A/B runs).
+    {
+        static const int beam_min = [] {
+            const char *s = std::getenv("RT_BEAM_MIN");
+            return s ? std::atoi(s) : BEAM_MIN_SPHERES;
+        }();
+        h.beam_ok = h.cull_ok && h.n_sph >= beam_min ? 1 : 0;
     }
     if (t.empty()) t.push_back(0);
 
