@@ -49,7 +49,7 @@ constexpr int BLOCK = 256; // 4 waves, 16x16 pixels
 
 // Occupancy target (waves per SIMD); the default is chosen by measurement.
 #ifndef RT_WAVES_PER_SIMD
-#define RT_WAVES_PER_SIMD 5
+#define RT_WAVES_PER_SIMD 4
 #endif
 #if RT_WAVES_PER_SIMD > 0
 #define RT_LAUNCH_BOUNDS __launch_bounds__(256, RT_WAVES_PER_SIMD)
@@ -1726,11 +1726,11 @@ int launch_frame(rt_prepared *p, const long long (&args)[12], hipStream_t st, F 
     return RT_OK;
 }
 
-// Engine.  Small scenes are bound by per-level latency (every level of the wavefront pipeline
-// costs its kernels' fixed ramp-up) and run fastest as the single fused kernel; larger ones by
-// the scans, where the wavefront pipeline's coherent waves and overlap win.  Measured on
-// MI355X at 4096^2 depth 5: fused ahead up to 32 spheres (S4 74 vs 56 Gpx/s, S32 34.7 vs
-// 33.0), wavefront ahead from 48 (S48 21.6 vs 20.7, S64 18.6 vs 15.6, S256 d8 4.2 vs 1.7).
+// Engine.  Small mixed scenes are bound by per-level latency (every level of the wavefront
+// pipeline costs its kernels' fixed ramp-up) and run fastest as the single fused kernel
+// (default scene 1920x1080 d5: 15.1 vs 6.1 Gpx/s); larger ones by the scans, where the wavefront
+// pipeline's coherent waves and overlap win (round 1, 4096^2 d5: wavefront ahead from 48
+// objects), and spheres-only scenes with LDS-staged tables at any size (below).
 // RT_ENGINE=fused | wave forces one; RT_FUSED_MAX_OBJECTS moves the crossover.
 constexpr int FUSED_MAX_OBJECTS = 40;
 bool use_mega_engine(const rt_prepared *p) {
@@ -1745,7 +1745,12 @@ bool use_mega_engine(const rt_prepared *p) {
         return s ? std::atoi(s) : FUSED_MAX_OBJECTS;
     }();
     if (mode) return mode == 1;
-    return p->hdr.n_obj <= max_obj;
+    // spheres-only scenes whose tables are staged in LDS: the wavefront engine at every size
+    // (measured round 2, 4096^2 d5, 4 frames in flight: S4 115 vs 89 Gpx/s, S8 86 vs 70,
+    // S16 58 vs 42, S24 49 vs 37, S32 52 vs 38)
+    const SceneHdr &h = p->hdr;
+    if (h.n_tri == 0 && h.n_pl == 0 && h.cull_ok && h.l_bytes > 0) return false;
+    return h.n_obj <= max_obj;
 }
 
 } // namespace
