@@ -1470,9 +1470,31 @@ int grow(void **buf, size_t *have, size_t need, unsigned *gen) {
     return RT_OK;
 }
 
+// Each level's shading fused into the next reflection pass (k_reflect_shade) when the context runs
+// without side streams; RT_FUSE_SHADE=0 keeps separate k_light launches, for A/B runs.
+bool fuse_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("RT_FUSE_SHADE");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
+// Does a wavefront pass write every pixel exactly once?  Yes with k_reflect_shade (the colours of
+// records with a reflection hit are left to k_walk) and without reflections; no when k_light
+// shades level 0 provisionally beside the chain (side streams, or levels requested).
+bool wave_single_write(const rt_prepared *p, int D, bool levels) {
+    const int nrefl = (p->hdr.n_light > 0 && D > 1) ? D - 1 : 0;
+    const bool overlap = lit_overlap(p) && D > 1 && p->hdr.n_light > 0;
+    return nrefl == 0 || (fuse_on() && !overlap && !levels);
+}
+
+// acc (slab row 0, binary64, or null): supersampled passes fold their sample into it where each
+// pixel is written (put_pixel) — only valid when wave_single_write holds.
 template <int PREC, bool GENPOW>
 int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns, int row_begin, int row_end, void *out,
-                     uint8_t *levels, hipStream_t st, int spp = 1, int sample = 0, unsigned long long seed = 0) {
+                     uint8_t *levels, hipStream_t st, int spp = 1, int sample = 0, unsigned long long seed = 0,
+                     double *acc = nullptr) {
     // renders slab rows [row_begin, row_end) (row_begin a multiple of TILE); out / levels point at slab row 0
     const int slab_rows = row_end - row_begin;
     const int nlev = D > 0 ? D : 1;
@@ -1518,12 +1540,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     const bool staged = sph_only && stage_env && p->hdr.l_bytes > 0;
     const size_t lds = staged ? (size_t)p->hdr.l_bytes : 0;
     // no side streams (frames in flight): each level's shading fused into the next reflection
-    // pass (k_reflect_shade); RT_FUSE_SHADE=0 keeps separate k_light launches, for A/B runs
-    static const bool fuse_env = [] {
-        const char *e = std::getenv("RT_FUSE_SHADE");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    const bool fuse = fuse_env && !overlap && !levels && nrefl > 0;
+    // pass (k_reflect_shade)
+    const bool fuse = fuse_on() && !overlap && !levels && nrefl > 0;
     for (int row0 = row_begin; row0 < row_end; row0 += pass_rows) {
         const int rows = std::min(pass_rows, row_end - row0);
         const int ntiles = tiles_x * ((rows + TILE - 1) / TILE);
@@ -1532,6 +1550,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         const size_t off = (size_t)row0 * W;
         void *o = static_cast<char *>(out) + off * 3 * (PREC == RT_OUT_F64 ? 8 : 4);
         uint8_t *lv = levels ? levels + off : nullptr;
+        double *acc_p = acc ? acc + off * 3 : nullptr;
         auto qk = [&](int k) { return q + (size_t)k * ntiles * TILE_SLOTS; };
         auto ck = [&](int k) { return p->d_counts + (size_t)k * ntiles; };
         int *nitems = p->d_items; // [0, 64): per-level record counts
@@ -1541,16 +1560,16 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         auto litk = [&](int k) { return p->d_lit + (size_t)k * ntiles * TILE_SLOTS; };
         HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
-        const PassGeom g{W, H, rb, sh, ns, row0, spp, sample, seed}; // level-0 records are rebuilt from it
+        const PassGeom g{W, H, rb, sh, ns, row0, spp, sample, seed, acc_p}; // level-0 records are rebuilt from it
         dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
         {
             KtScope kt(p, RT_KT_PRIMARY, st);
             if (lv)
                 hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W,
-                                   H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed);
+                                   H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed, acc_p);
             else
                 hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
-                                   W, H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed);
+                                   W, H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed, acc_p);
         }
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
@@ -1814,10 +1833,21 @@ int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dep
         const int blocks = (int)std::min<size_t>(8192, (n + 255) / 256);
         void *dst = static_cast<char *>(d_out) + e0 * (precision == RT_OUT_F64 ? 8 : 4);
         for (int s = 0; s < (int)spp; ++s) {
-            rc = p->hdr.int_pow ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, r0, r1, smp,
-                                                                      s == 0 ? d_levels : nullptr, st, (int)spp, s, seed)
-                                : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, r0, r1, smp,
-                                                                     s == 0 ? d_levels : nullptr, st, (int)spp, s, seed);
+            uint8_t *lv = s == 0 ? d_levels : nullptr;
+            if (wave_single_write(p, D, lv != nullptr)) {
+                // every pixel written once: the pass folds its sample into acc (and the last one
+                // writes the output) itself — no sample slab, no k_accum
+#define RT_SS(P) (p->hdr.int_pow ? launch_wavefront<P, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, nullptr, st, (int)spp, s, seed, acc) \
+                                 : launch_wavefront<P, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, nullptr, st, (int)spp, s, seed, acc))
+                rc = precision == RT_OUT_F64 ? RT_SS(RT_OUT_F64) : RT_SS(RT_OUT_F32);
+#undef RT_SS
+                if (rc != RT_OK) return rc;
+                continue;
+            }
+            rc = p->hdr.int_pow ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, r0, r1, smp, lv, st,
+                                                                      (int)spp, s, seed)
+                                : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, r0, r1, smp, lv, st,
+                                                                     (int)spp, s, seed);
             if (rc != RT_OK) return rc;
             if (precision == RT_OUT_F64)
                 hipLaunchKernelGGL(k_accum<RT_OUT_F64>, dim3(blocks), dim3(256), 0, st, n, smp + e0, acc + e0, dst, s,

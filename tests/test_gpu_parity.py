@@ -239,6 +239,39 @@ def test_supersampling_shards():
         L.rt_release(p)
 
 
+@pytest.mark.parametrize("name,w,h,d,spp", [("s64", 48, 40, 5, 4), ("default", 40, 37, 5, 3), ("s256", 32, 24, 8, 16),
+                                            ("mixed", 40, 32, 4, 2), ("s64", 33, 21, 1, 3), ("s64", 24, 16, 0, 2)])
+def test_supersampling_single_write_path(name, w, h, d, spp):
+    """Without side streams each pass writes every pixel once and folds its sample into the
+    running sum where it writes (no sample slab, no k_accum): bit for bit the frame of the
+    sample-slab path (side streams on), f64 and f32, and no row past the image written."""
+    import torch
+    L = N.lib()
+    el = N.marshal(scenes.named(name))
+    st = torch.cuda.current_stream().cuda_stream
+    rb, seed = 16, 0x5EED0005
+    frames = {}
+    for side in (1, 0):
+        p = ctypes.c_void_p()
+        N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(p)), "rt_prepare")
+        try:
+            N.check(L.rt_configure(p, N.RT_CFG_SIDE_STREAMS, side))
+            for prec, dt in ((N.RT_OUT_F64, torch.float64), (N.RT_OUT_F32, torch.float32)):
+                buf = torch.full((h + 16, w, 3), 12345.0, dtype=dt, device="cuda")
+                for _ in range(2):  # a second frame reuses the running sum: no state leaks between frames
+                    N.check(L.rt_launch_spp(p, w, h, d, rb, 0, 1, prec, N.RT_ORDER_EXACT, spp, seed, buf.data_ptr(),
+                                            None, st))
+                torch.cuda.synchronize()
+                assert bool((buf[h:] == 12345.0).all())
+                frames[side, prec] = buf[:h].cpu()
+        finally:
+            L.rt_release(p)
+    for prec in (N.RT_OUT_F64, N.RT_OUT_F32):
+        a, b = frames[1, prec], frames[0, prec]
+        assert torch.equal(a.view(torch.int64 if a.dtype == torch.float64 else torch.int32),
+                           b.view(torch.int64 if b.dtype == torch.float64 else torch.int32)), (name, prec)
+
+
 # ---- P3 output on the GPU (write_pixels_to_ppm/5, raytracer.erl:667-685) ---------------------
 
 def _py_ppm(tmp_path, img, maxv=255):
