@@ -550,7 +550,11 @@ __device__ __forceinline__ void scan_tri_pl(const Scene &S, int org, const D3 &o
     }
 }
 
-constexpr int MAX_GROUPS = 3;
+#ifndef RT_MAX_GROUPS
+#define RT_MAX_GROUPS 3 // reflection beams per wave (lanes grouped by the object they leave)
+#endif
+constexpr int MAX_GROUPS = RT_MAX_GROUPS;
+constexpr int UNION_CHUNKS = 4; // reflection scans of scenes up to 256 spheres walk the union of the groups' candidates
 template <bool PRE, bool ILP = false, int SPH = 0>
 __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, bool act,
                                        int grp = -1) {
@@ -562,10 +566,14 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
     RT_STAT(PRE ? ST_NEAR_PRE : ST_NEAR_GEN, 1);
     RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
     unsigned long long rem = __ballot(act);
-    if (!PRE && h.n_sph <= 64) {
-        // One chunk: the union of the groups' candidate masks, walked once by the whole wave
-        // (a sphere outside a lane's cone cannot be hit by that lane, so testing it is harmless).
-        unsigned long long m = 0;
+    // staged (SPH = 2) scans keep the single-chunk form (S64: fewer registers, measured faster)
+    constexpr int UCH = SPH == 2 ? 1 : UNION_CHUNKS;
+    if (!PRE && h.n_sph <= 64 * UCH) {
+        // The union of the groups' candidate masks (per 64-sphere chunk), walked once by the whole
+        // wave (a sphere outside a lane's cone cannot be hit by that lane, so testing it is
+        // harmless): each candidate is tested once however many groups share it.
+        unsigned long long m[UCH] = {};
+        const int nch = (h.n_sph + 63) >> 6;
         bool all = false;
         for (int g = 0; g < MAX_GROUPS && rem; ++g) {
             const int gv = __builtin_amdgcn_readlane(grp, __builtin_ctzll(rem));
@@ -577,10 +585,13 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
                 all = true;
                 break;
             }
-            m |= cull_chunk<SPH>(S, b, 0, -1);
+#pragma unroll
+            for (int c = 0; c < UCH; ++c)
+                if (c < nch) m[c] |= cull_chunk<SPH>(S, b, c * 64, -1);
         }
-        if (all) m = chunk_all(h.n_sph, 0);
-        scan_spheres<false, ILP>(S, org, o, d, A4, 0, m, bt, bid);
+#pragma unroll
+        for (int c = 0; c < UCH; ++c)
+            if (c < nch) scan_spheres<false, ILP>(S, org, o, d, A4, c * 64, all ? chunk_all(h.n_sph, c * 64) : m[c], bt, bid);
         rem = 0;
     }
     for (int g = 0; g < MAX_GROUPS && rem; ++g) {
