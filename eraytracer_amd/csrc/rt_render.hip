@@ -1646,17 +1646,27 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             HIPCHK(hipGetLastError());
             if ((rc = level_lists(k)) != RT_OK) return rc;
         }
-        // deep levels (see deep_dense): k_walk_deep right after the chain; the chains ending at
-        // level 1 (the bulk) are finished on side stream 0 as soon as levels 0 and 1 are
+        // Without side streams one k_walk finishes every chain (sparse deep levels shaded on the
+        // way).  With side streams (see deep_dense): k_walk_deep right after the chain; the chains
+        // ending at level 1 (the bulk) are finished on side stream 0 as soon as levels 0 and 1 are
         // shaded, beside it; then the rest, once every level's shading is in (side stream 1
         // shades levels 1.. in order: its last level's event covers them all)
         if (nrefl > 0) {
             const size_t ls_ = (size_t)ntiles * TILE_SLOTS;
             const bool bits = p->hdr.n_light <= 32; // the shadow answers fit the record
-            auto walk = [&](hipStream_t s_, int lo, int hi) {
+            // deep: the merged walk (no k_walk_deep; without side streams)
+            auto walk = [&](hipStream_t s_, int lo, int hi, bool deep) {
 #define RT_WALK(SPHV, BITSV, LDSV)                                                                                  \
-    hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV>), dim3(sblocks), dim3(BLOCK), LDSV, s_, p->hdr, p->d_tab, \
-                       p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child, p->d_lit, lo, hi, g)
+    do {                                                                                                           \
+        if (deep)                                                                                                  \
+            hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV, true>), dim3(sblocks), dim3(BLOCK), LDSV, s_,     \
+                               p->hdr, p->d_tab, p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf,      \
+                               p->d_child, p->d_lit, lo, hi, g);                                                    \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV, false>), dim3(sblocks), dim3(BLOCK), LDSV, s_,    \
+                               p->hdr, p->d_tab, p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf,      \
+                               p->d_child, p->d_lit, lo, hi, g);                                                    \
+    } while (0)
                 if (staged && bits) RT_WALK(2, true, lds);
                 else if (staged) RT_WALK(2, false, lds);
                 else if (sph_only && bits) RT_WALK(1, true, 0);
@@ -1669,11 +1679,11 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                            // k_reflect(2), which marks the level-1 records that have a child
                 HIPCHK(hipStreamWaitEvent(p->side[0], p->ev_lit[1], 0));
                 if (D > 2) HIPCHK(hipStreamWaitEvent(p->side[0], p->ev_level[2], 0));
-                walk(p->side[0], 1, 2);
+                walk(p->side[0], 1, 2, false);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipEventRecord(p->ev_lit[0], p->side[0]));
             }
-            if (D > 2) {
+            if (D > 2 && overlap) {
                 if (staged)
                     hipLaunchKernelGGL((k_walk_deep<GENPOW, 2>), dim3(sblocks), dim3(BLOCK), lds, st, p->hdr,
                                        p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, colk(2));
@@ -1688,9 +1698,9 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             if (overlap) {
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[nrefl], 0));
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
-                if (D > 2) walk(st, 2, D);
+                if (D > 2) walk(st, 2, D, false);
             } else {
-                walk(st, 1, D); // every chain in one launch (levels 2.. after k_walk_deep)
+                walk(st, 1, D, true); // every chain in one launch, sparse deep levels shaded there too
             }
             HIPCHK(hipGetLastError());
         } else if (overlap && nshade > 0) {
