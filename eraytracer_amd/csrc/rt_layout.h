@@ -45,6 +45,18 @@ constexpr int OBJ_META_W = 4; // kind, local index within its type, canon compac
 
 constexpr int LDS_STAGE_MAX = 32 * 1024; // 5 workgroups per CU keep their 32 KiB each
 
+// Sphere BVH for incoherent reflection rays (see rt_render.hip, "Per-lane BVH"): a binary tree
+// over the spheres, built on the host by median splits (depth = ceil(log2 n_sph)); one 64-byte
+// node holds both children's binary32 boxes (rounded outwards and inflated, so the box test
+// never rejects a sphere the binary64 test accepts), their links (>= 0: node, < 0: ~sphere) and,
+// for a sphere child, the sphere's compact object id.
+constexpr int BVH_NODE_DOUBLES = 8;  // 64 bytes
+constexpr int BVH_LDS_MAX = 40 * 1024; // nodes + sphere rows staged in LDS up to this size
+constexpr int BVH_STACK = 12;        // per-lane traversal stack entries (tree depth <= BVH_STACK: 4096 spheres)
+constexpr int BVH_MIN_SPHERES = 128; // below this the wave beams are cheaper (default; RT_BVH_MIN)
+constexpr int BVH_LEVEL = 2;         // first reflection level traversing the BVH (default; RT_BVH_LEVEL)
+constexpr double BVH_BOX_REL = 1.0e-5; // box inflation, relative to the scene extent (+1)
+
 enum ObjKind : int { K_SPHERE = 0, K_TRIANGLE = 1, K_PLANE = 2 };
 
 // Scalar header passed to the kernel by value.  All offsets index the double table `tab`
@@ -68,6 +80,12 @@ struct SceneHdr {
     // (o_sph_org from origin 1 on), the occluder masks (i_occ), the sphere ids (i_sph_id) and
     // the sphere bounds of the reflection rays' beam culling (o_sph_b).
     int l_obj, l_meta, l_org, l_occ, l_id, l_sphb, l_bytes;
+    // sphere BVH (bvh_ok: built and within its limits): nodes at tab[o_bvh], n_bvh of them, depth
+    // bvh_depth; the reflection scans of levels >= bvh_level traverse it per lane (the wave beams
+    // below that level).  Set per launch (the reflection kernels' dynamic LDS): byte offsets of the
+    // nodes and the sphere rows (o_sph) staged there (l_bvh = -1: read from HBM) and of each
+    // lane's stack (l_stack).
+    int bvh_ok, o_bvh, n_bvh, bvh_level, bvh_depth, l_bvh, l_bsph, l_stack;
     // camera (point_on_screen/3, :486-503, with focal_length/2 :483-484 folded in)
     double cam_x, cam_y, cam_z; // Camera#camera.location
     double sx;   // 0*F + Lx            (first fold step, x)

@@ -303,7 +303,8 @@ __device__ unsigned long long g_stats[16];
     } while (0)
 #endif
 enum { ST_WAVES, ST_NEAR_PRE, ST_NEAR_PRE_CAND, ST_NEAR_GEN, ST_NEAR_GEN_CAND, ST_SHADOW, ST_SHADOW_CAND,
-       ST_SHADOW_ITER, ST_SHADE, ST_SHADOW_CONE_ON, ST_BEAM_ON, ST_SHADOW_LANES, ST_NEAR_LANES };
+       ST_SHADOW_ITER, ST_SHADE, ST_SHADOW_CONE_ON, ST_BEAM_ON, ST_SHADOW_LANES, ST_NEAR_LANES, ST_BVH_SCANS,
+       ST_BVH_ITER, ST_BVH_LEAF };
 
 // ---- Beam culling ----------------------------------------------------------------------------
 // A wave's 64 rays are coherent (an 8x8 pixel tile; shadow rays of one light; their
@@ -550,6 +551,116 @@ __device__ __forceinline__ void scan_tri_pl(const Scene &S, int org, const D3 &o
     }
 }
 
+// ---- Per-lane BVH (incoherent reflection rays) ------------------------------------------------
+// Deep reflection levels of large scenes leave every wave's rays pointing everywhere: a wave
+// beam then keeps most spheres (S256 depth 8: ~200 of 256 candidates per scan).  Those scans
+// walk the host-built sphere BVH instead, each lane on its own ray (ordered traversal: both
+// children's boxes tested, the nearer visited first, the other pushed with its entry distance).
+// The box tests are binary32 slab tests on boxes rounded outwards and inflated (rt_scene.cpp), a
+// conservative filter with a relative tolerance of 2^-16 on every distance compared; a sphere
+// leaf that passes is tested with the reference's binary64 expressions (sphere_BC + sph_t), and
+// the (t, list position) minimum does not depend on the visiting order, so the result is the
+// candidate walk's.  Each lane's stack holds (entry distance rounded down to bfloat16, node) in
+// one word, in LDS (BVH_STACK words per lane, lane-interleaved: no bank conflicts).
+__device__ __forceinline__ float bvh_inv(double d) {
+    float f = (float)d;
+    f = fabsf(f) < 1.0e-30f ? copysignf(1.0e-30f, f) : f; // no inf * 0 in the slab test
+    return __builtin_amdgcn_rcpf(f);                       // ~1 ulp: inside the tolerance
+}
+struct BvhRay {
+    float ox, oy, oz, ix, iy, iz;
+};
+// [tn, tx] of box (l, u) along the ray, clipped to [0, tlim]; true if they overlap (tolerant)
+__device__ __forceinline__ bool bvh_slab(const BvhRay &r, float lx, float ly, float lz, float ux, float uy, float uz,
+                                         float tlim, float &tn) {
+    constexpr float LO = 1.0f - 0x1p-16f, HI = 1.0f + 0x1p-16f;
+    const float ax = (lx - r.ox) * r.ix, bx = (ux - r.ox) * r.ix;
+    const float ay = (ly - r.oy) * r.iy, by = (uy - r.oy) * r.iy;
+    const float az = (lz - r.oz) * r.iz, bz = (uz - r.oz) * r.iz;
+    tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+    const float tx = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tlim));
+    return tn * LO <= tx * HI;
+}
+// Stage the BVH nodes and the sphere rows in this workgroup's LDS (every thread of the block,
+// before any traversal) when the launch placed them there (l_bvh >= 0).
+__device__ __forceinline__ void stage_bvh(const Scene &S) {
+    const SceneHdr &h = S.h;
+    if (h.l_bvh < 0) return;
+    const int4 *sn = reinterpret_cast<const int4 *>(S.tab + h.o_bvh);
+    int4 *dn = reinterpret_cast<int4 *>(g_lds + h.l_bvh);
+    for (int i = threadIdx.x; i < h.n_bvh * 4; i += blockDim.x) dn[i] = sn[i];
+    const int4 *ss = reinterpret_cast<const int4 *>(S.tab + h.o_sph);
+    int4 *ds = reinterpret_cast<int4 *>(g_lds + h.l_bsph);
+    for (int i = threadIdx.x; i < h.n_sph * 2; i += blockDim.x) ds[i] = ss[i];
+    __syncthreads();
+}
+// LDS: the nodes and sphere rows are staged in LDS (h.l_bvh >= 0), else read from HBM (L2)
+template <bool LDS>
+__device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &d, double A4, bool act, double &bt,
+                                         int &bid) {
+    const SceneHdr &h = S.h;
+    const float4 *nodes = LDS ? reinterpret_cast<const float4 *>(g_lds + h.l_bvh)
+                              : reinterpret_cast<const float4 *>(S.tab + h.o_bvh);
+    const double2 *rows = LDS ? reinterpret_cast<const double2 *>(g_lds + h.l_bsph)
+                              : reinterpret_cast<const double2 *>(S.tab + h.o_sph);
+    unsigned *stk = reinterpret_cast<unsigned *>(g_lds + h.l_stack) + (threadIdx.x >> 6) * (64 * h.bvh_depth) +
+                    (threadIdx.x & 63);
+    const BvhRay ray{(float)o.x, (float)o.y, (float)o.z, bvh_inv(d.x), bvh_inv(d.y), bvh_inv(d.z)};
+    constexpr float HI = 1.0f + 0x1p-16f;
+    float tlim = __builtin_inff();
+    // sphere k (local index, compact id id), as sphere_BC<false> + sph_t (the candidate walk's
+    // expressions)
+    auto leaf = [&](int k, int id) {
+        RT_STAT(ST_BVH_LEAF, 1);
+        const double2 c01 = rows[k * 2], c2r = rows[k * 2 + 1];
+        const D3 oc = {o.x - c01.x, o.y - c01.y, o.z - c2r.x};
+        const double B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
+        const double C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - c2r.y;
+        double t;
+        if (sph_t(B, C, A4, t) && nearer(t, id, bt, bid)) {
+            bt = t;
+            bid = id;
+            tlim = (float)t * HI;
+        }
+    };
+    int node = act ? 0 : -1, sp = 0;
+    RT_STAT(ST_BVH_SCANS, 1);
+    while (node >= 0) {
+        RT_STAT(ST_BVH_ITER, 1);
+        const float4 a = nodes[node * 4], b = nodes[node * 4 + 1], c = nodes[node * 4 + 2], e = nodes[node * 4 + 3];
+        float tn0, tn1;
+        bool h0 = bvh_slab(ray, a.x, a.y, a.z, a.w, b.x, b.y, tlim, tn0);
+        bool h1 = bvh_slab(ray, b.z, b.w, c.x, c.y, c.z, c.w, tlim, tn1);
+        const int c0 = __float_as_int(e.x), c1 = __float_as_int(e.y);
+        if (h0 && c0 < 0) {
+            leaf(~c0, __float_as_int(e.z));
+            h0 = false;
+        }
+        if (h1 && c1 < 0) {
+            leaf(~c1, __float_as_int(e.w));
+            h1 = false;
+        }
+        if (h0 && h1) {
+            const bool f0 = tn0 <= tn1;
+            const float tf = f0 ? tn1 : tn0;
+            stk[sp * 64] = (__float_as_uint(tf) & 0xffff0000u) | (unsigned)(f0 ? c1 : c0); // tf >= 0: truncation rounds down
+            ++sp;
+            node = f0 ? c0 : c1;
+        } else if (h0 | h1) {
+            node = h0 ? c0 : c1;
+        } else {
+            node = -1;
+            while (sp > 0) {
+                const unsigned en = stk[--sp * 64];
+                if (__uint_as_float(en & 0xffff0000u) <= tlim) {
+                    node = (int)(en & 0xffffu);
+                    break;
+                }
+            }
+        }
+    }
+}
+
 #ifndef RT_MAX_GROUPS
 #define RT_MAX_GROUPS 3 // reflection beams per wave (lanes grouped by the object they leave)
 #endif
@@ -557,7 +668,7 @@ constexpr int MAX_GROUPS = RT_MAX_GROUPS;
 constexpr int UNION_CHUNKS = 4; // reflection scans of scenes up to 256 spheres walk the union of the groups' candidates
 template <bool PRE, bool ILP = false, int SPH = 0>
 __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, bool act,
-                                       int grp = -1) {
+                                       int grp = -1, bool bvh = false) {
     const SceneHdr &h = S.h;
     bt = __builtin_inf();
     int bid = 0x7fffffff;
@@ -565,6 +676,14 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
     const double A4 = 4 * (d.x * d.x + d.y * d.y + d.z * d.z);
     RT_STAT(PRE ? ST_NEAR_PRE : ST_NEAR_GEN, 1);
     RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
+    if (!PRE && bvh) { // (wave-uniform) per-lane BVH traversal, then the triangles and planes
+        if (h.l_bvh >= 0)
+            scan_bvh<true>(S, o, d, A4, act, bt, bid);
+        else
+            scan_bvh<false>(S, o, d, A4, act, bt, bid);
+        scan_tri_pl<PRE>(S, org, o, d, bt, bid);
+        return (act && bid != 0x7fffffff) ? bid : -1;
+    }
     unsigned long long rem = __ballot(act);
     // staged (SPH = 2) scans keep the single-chunk form (S64: fewer registers, measured faster)
     constexpr int UCH = SPH == 2 ? 1 : UNION_CHUNKS;
@@ -1550,6 +1669,21 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     }();
     const bool staged = sph_only && stage_env && p->hdr.l_bytes > 0;
     const size_t lds = staged ? (size_t)p->hdr.l_bytes : 0;
+    // Reflection kernels of levels that traverse the sphere BVH: after the staged tables in LDS,
+    // the BVH nodes and sphere rows (when they fit BVH_LDS_MAX) and every lane's stack.
+    SceneHdr rhdr = p->hdr;
+    size_t lds_bvh = lds;
+    if (rhdr.bvh_ok) {
+        const size_t nb = (size_t)rhdr.n_bvh * BVH_NODE_DOUBLES * 8, sb = (size_t)rhdr.n_sph * SPH_W * 8;
+        if (nb + sb <= (size_t)BVH_LDS_MAX) {
+            rhdr.l_bvh = (int)lds_bvh;
+            rhdr.l_bsph = (int)(lds_bvh + nb);
+            lds_bvh += nb + sb;
+        }
+        rhdr.l_stack = (int)lds_bvh;
+        lds_bvh += (size_t)BLOCK * rhdr.bvh_depth * sizeof(unsigned);
+    }
+    auto lds_r = [&](int k) { return rhdr.bvh_ok && k >= rhdr.bvh_level ? lds_bvh : lds; };
     // no side streams (frames in flight): each level's shading fused into the next reflection
     // pass (k_reflect_shade)
     const bool fuse = fuse_on() && !overlap && !levels && nrefl > 0;
@@ -1621,27 +1755,27 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             KtScope kt(p, k == 1 ? RT_KT_LEVEL1 : 0, st);
             if (fuse) {
 #define RT_RS(SPHV, ILPV, LDSV)                                                                                     \
-    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV>), dim3(sblocks), dim3(BLOCK), LDSV, st, p->hdr,        \
+    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV>), dim3(sblocks), dim3(BLOCK), LDSV, st, rhdr,         \
                        p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
                        colk(k - 1), litk(k - 1), g)
-                if (staged && k == 1) RT_RS(2, false, lds);
-                else if (staged) RT_RS(2, true, lds);
-                else if (sph_only && k == 1) RT_RS(1, false, 0);
-                else if (sph_only) RT_RS(1, true, 0);
-                else if (k == 1) RT_RS(0, false, 0);
-                else RT_RS(0, true, 0);
+                if (staged && k == 1) RT_RS(2, false, lds_r(k));
+                else if (staged) RT_RS(2, true, lds_r(k));
+                else if (sph_only && k == 1) RT_RS(1, false, lds_r(k));
+                else if (sph_only) RT_RS(1, true, lds_r(k));
+                else if (k == 1) RT_RS(0, false, lds_r(k));
+                else RT_RS(0, true, lds_r(k));
 #undef RT_RS
             } else if (lv && k == 1)
-                hipLaunchKernelGGL((k_reflect<true, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                hipLaunchKernelGGL((k_reflect<true, false>), dim3(sblocks), dim3(BLOCK), lds_r(k), st, rhdr, p->d_tab,
                                    p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             else if (lv)
-                hipLaunchKernelGGL((k_reflect<true, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                hipLaunchKernelGGL((k_reflect<true, true>), dim3(sblocks), dim3(BLOCK), lds_r(k), st, rhdr, p->d_tab,
                                    p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             else if (k == 1)
-                hipLaunchKernelGGL((k_reflect<false, false>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                hipLaunchKernelGGL((k_reflect<false, false>), dim3(sblocks), dim3(BLOCK), lds_r(k), st, rhdr, p->d_tab,
                                    p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             else
-                hipLaunchKernelGGL((k_reflect<false, true>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr, p->d_tab,
+                hipLaunchKernelGGL((k_reflect<false, true>), dim3(sblocks), dim3(BLOCK), lds_r(k), st, rhdr, p->d_tab,
                                    p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             HIPCHK(hipGetLastError());
             if ((rc = level_lists(k)) != RT_OK) return rc;

@@ -4,6 +4,7 @@
 // Every precomputed quantity is produced with the reference's operation order, in IEEE
 // binary64, compiled with -ffp-contract=off, so the kernel sees bit-identical values to
 // those the reference computes per ray.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -91,6 +92,143 @@ int fill_canon(rt_elem *e, uint32_t n) {
 static int root(const std::vector<rt_elem> &e, int i) {
     while (e[i].canon >= 0 && e[i].canon != i) i = e[i].canon;
     return i;
+}
+
+// binary32 bounds that contain the binary64 value: rounded down (lo) or up (hi)
+static float f32_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = std::nextafterf(f, -INFINITY);
+    return f;
+}
+static float f32_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = std::nextafterf(f, INFINITY);
+    return f;
+}
+
+// Sphere BVH for the reflection scans (rt_layout.h).  Median splits along the longest axis of
+// the centroids' bounds, so the depth is ceil(log2 n) and the per-lane stack never overflows.
+// Each sphere's box is its centre +- |r| widened by m = BVH_BOX_REL * (extent + 1), far more than
+// the binary32 rounding of the kernel's slab test (origins and directions rounded to binary32,
+// relative error ~2^-22 in the slab distances) for scenes within CULL_EXTENT; the box test is only
+// a filter, every sphere it lets through is tested by the reference's binary64 expressions.
+static void build_bvh(const std::vector<rt_elem> &e, const std::vector<int> &sph, const std::vector<int> &compact,
+                      const std::vector<rt_vec3> &org, SceneHdr &h, std::vector<double> &t) {
+    h.bvh_ok = 0;
+    h.o_bvh = 0;
+    h.n_bvh = 0;
+    h.bvh_level = 1 << 30;
+    h.bvh_depth = 0;
+    h.l_bvh = h.l_bsph = -1;
+    h.l_stack = 0;
+    static const int bvh_min = [] {
+        const char *s = std::getenv("RT_BVH_MIN");
+        return s ? std::atoi(s) : BVH_MIN_SPHERES;
+    }();
+    static const int bvh_level = [] {
+        const char *s = std::getenv("RT_BVH_LEVEL");
+        return s ? std::atoi(s) : BVH_LEVEL; // level 1 (coherent: from the primary hits) keeps the beams
+    }();
+    const int n = (int)sph.size();
+    if (!h.cull_ok || n < 2 || n < bvh_min) return;
+    int depth = 0;
+    while ((1 << depth) < n) ++depth;
+    if (depth > BVH_STACK) return; // a node at depth i holds at most i stack entries, pushes one more
+    double ext = 0;
+    for (const rt_vec3 &o : org) ext = std::fmax(ext, std::fmax(std::fabs(o.x), std::fmax(std::fabs(o.y), std::fabs(o.z))));
+    for (int i : sph) {
+        const auto &s = e[i].u.sphere;
+        ext = std::fmax(ext, std::fmax(std::fabs(s.center.x), std::fmax(std::fabs(s.center.y), std::fabs(s.center.z))) +
+                                 std::fabs(s.radius));
+    }
+    const double m = BVH_BOX_REL * (ext + 1.0);
+    struct Box {
+        double lo[3], hi[3];
+    };
+    auto sbox = [&](int k) {
+        const auto &s = e[sph[k]].u.sphere;
+        const double c[3] = {s.center.x, s.center.y, s.center.z}, r = std::fabs(s.radius);
+        Box b;
+        for (int a = 0; a < 3; ++a) {
+            b.lo[a] = c[a] - r - m;
+            b.hi[a] = c[a] + r + m;
+        }
+        return b;
+    };
+    struct Node {
+        Box b[2];
+        int ch[2];
+    };
+    std::vector<Node> nodes;
+    nodes.reserve(n);
+    std::vector<int> items(n);
+    for (int k = 0; k < n; ++k) items[k] = k;
+    // returns the link of the subtree over items[b, e) and its box
+    auto build = [&](auto &&self, int b, int en, Box &box) -> int {
+        if (en - b == 1) {
+            box = sbox(items[b]);
+            return ~items[b];
+        }
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = b; i < en; ++i) {
+            const auto &s = e[sph[items[i]]].u.sphere;
+            const double c[3] = {s.center.x, s.center.y, s.center.z};
+            for (int a = 0; a < 3; ++a) {
+                clo[a] = std::fmin(clo[a], c[a]);
+                chi[a] = std::fmax(chi[a], c[a]);
+            }
+        }
+        int ax = 0;
+        for (int a = 1; a < 3; ++a)
+            if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
+        auto key = [&](int k) {
+            const auto &s = e[sph[k]].u.sphere;
+            return ax == 0 ? s.center.x : ax == 1 ? s.center.y : s.center.z;
+        };
+        std::sort(items.begin() + b, items.begin() + en, [&](int p, int q) {
+            const double kp = key(p), kq = key(q);
+            return kp < kq || (kp == kq && p < q);
+        });
+        const int mid = b + (en - b) / 2;
+        const int self_i = (int)nodes.size();
+        nodes.push_back(Node{});
+        Box bl, br;
+        const int l = self(self, b, mid, bl);
+        const int r = self(self, mid, en, br);
+        nodes[self_i].b[0] = bl;
+        nodes[self_i].b[1] = br;
+        nodes[self_i].ch[0] = l;
+        nodes[self_i].ch[1] = r;
+        for (int a = 0; a < 3; ++a) {
+            box.lo[a] = std::fmin(bl.lo[a], br.lo[a]);
+            box.hi[a] = std::fmax(bl.hi[a], br.hi[a]);
+        }
+        return self_i;
+    };
+    Box root;
+    build(build, 0, n, root);
+    while (t.size() % 2) t.push_back(0); // 16-byte aligned nodes
+    h.o_bvh = (int)t.size();
+    for (const Node &nd : nodes) {
+        float f[16];
+        const Box &b0 = nd.b[0], &b1 = nd.b[1];
+        f[0] = f32_down(b0.lo[0]); f[1] = f32_down(b0.lo[1]); f[2] = f32_down(b0.lo[2]);
+        f[3] = f32_up(b0.hi[0]); f[4] = f32_up(b0.hi[1]); f[5] = f32_up(b0.hi[2]);
+        f[6] = f32_down(b1.lo[0]); f[7] = f32_down(b1.lo[1]); f[8] = f32_down(b1.lo[2]);
+        f[9] = f32_up(b1.hi[0]); f[10] = f32_up(b1.hi[1]); f[11] = f32_up(b1.hi[2]);
+        std::memcpy(&f[12], &nd.ch[0], 4);
+        std::memcpy(&f[13], &nd.ch[1], 4);
+        const int id0 = nd.ch[0] < 0 ? compact[sph[~nd.ch[0]]] : -1, id1 = nd.ch[1] < 0 ? compact[sph[~nd.ch[1]]] : -1;
+        std::memcpy(&f[14], &id0, 4);
+        std::memcpy(&f[15], &id1, 4);
+        double d[BVH_NODE_DOUBLES];
+        std::memcpy(d, f, sizeof(d));
+        t.insert(t.end(), d, d + BVH_NODE_DOUBLES);
+    }
+    h.n_bvh = (int)nodes.size();
+    h.bvh_depth = depth;
+    h.bvh_ok = 1;
+    h.bvh_level = bvh_level < 1 ? 1 : bvh_level;
 }
 
 int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
@@ -267,6 +405,7 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
         }();
         h.beam_ok = h.cull_ok && h.n_sph >= beam_min ? 1 : 0;
     }
+    build_bvh(e, sph, compact, org, h, t);
     if (t.empty()) t.push_back(0);
 
     // int table
