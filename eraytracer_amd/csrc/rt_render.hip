@@ -47,6 +47,7 @@ namespace {
 
 constexpr int BLOCK = 256; // 4 waves, 16x16 pixels
 
+
 // Occupancy target (waves per SIMD); the default is chosen by measurement.
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
@@ -567,19 +568,42 @@ __device__ __forceinline__ float bvh_inv(double d) {
     f = fabsf(f) < 1.0e-30f ? copysignf(1.0e-30f, f) : f; // no inf * 0 in the slab test
     return __builtin_amdgcn_rcpf(f);                       // ~1 ulp: inside the tolerance
 }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 struct BvhRay {
-    float ox, oy, oz, ix, iy, iz;
+    f32x2 ix, iy, iz;    // 1 / d (binary32, both lanes of the pair)
+    f32x2 nox, noy, noz; // -(o * (1 / d))
 };
-// [tn, tx] of box (l, u) along the ray, clipped to [0, tlim]; true if they overlap (tolerant)
-__device__ __forceinline__ bool bvh_slab(const BvhRay &r, float lx, float ly, float lz, float ux, float uy, float uz,
-                                         float tlim, float &tn) {
+__device__ __forceinline__ BvhRay bvh_ray(const D3 &o, const D3 &d) {
+    BvhRay r;
+    const float ix = bvh_inv(d.x), iy = bvh_inv(d.y), iz = bvh_inv(d.z);
+    r.ix = f32x2{ix, ix};
+    r.iy = f32x2{iy, iy};
+    r.iz = f32x2{iz, iz};
+    r.nox = f32x2{-((float)o.x * ix), -((float)o.x * ix)};
+    r.noy = f32x2{-((float)o.y * iy), -((float)o.y * iy)};
+    r.noz = f32x2{-((float)o.z * iz), -((float)o.z * iz)};
+    return r;
+}
+// Slab tests of both children of a node: [tn, tx] of each box along the ray, clipped to [0, tlim];
+// h0/h1 true where they overlap (tolerant).  The distances are b * (1/d) - o * (1/d) (one packed fma
+// per axis and bound); its cancellation error, <= 2^-23 * extent * |1/d|, is far inside the boxes'
+// inflation (BVH_BOX_REL * (extent + 1) in space, i.e. that times |1/d| in distance).
+__device__ __forceinline__ void bvh_slab2(const BvhRay &r, const float4 &a, const float4 &b, const float4 &c, float tlim,
+                                          bool &h0, float &tn0, bool &h1, float &tn1) {
     constexpr float LO = 1.0f - 0x1p-16f, HI = 1.0f + 0x1p-16f;
-    const float ax = (lx - r.ox) * r.ix, bx = (ux - r.ox) * r.ix;
-    const float ay = (ly - r.oy) * r.iy, by = (uy - r.oy) * r.iy;
-    const float az = (lz - r.oz) * r.iz, bz = (uz - r.oz) * r.iz;
-    tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
-    const float tx = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tlim));
-    return tn * LO <= tx * HI;
+    const f32x2 tlx = __builtin_elementwise_fma(f32x2{a.x, a.y}, r.ix, r.nox);
+    const f32x2 tly = __builtin_elementwise_fma(f32x2{a.z, a.w}, r.iy, r.noy);
+    const f32x2 tlz = __builtin_elementwise_fma(f32x2{b.x, b.y}, r.iz, r.noz);
+    const f32x2 tux = __builtin_elementwise_fma(f32x2{b.z, b.w}, r.ix, r.nox);
+    const f32x2 tuy = __builtin_elementwise_fma(f32x2{c.x, c.y}, r.iy, r.noy);
+    const f32x2 tuz = __builtin_elementwise_fma(f32x2{c.z, c.w}, r.iz, r.noz);
+    tn0 = fmaxf(fmaxf(fminf(tlx.x, tux.x), fminf(tly.x, tuy.x)), fmaxf(fminf(tlz.x, tuz.x), 0.0f));
+    tn1 = fmaxf(fmaxf(fminf(tlx.y, tux.y), fminf(tly.y, tuy.y)), fmaxf(fminf(tlz.y, tuz.y), 0.0f));
+    const float tx0 = fminf(fminf(fmaxf(tlx.x, tux.x), fmaxf(tly.x, tuy.x)), fminf(fmaxf(tlz.x, tuz.x), tlim));
+    const float tx1 = fminf(fminf(fmaxf(tlx.y, tux.y), fmaxf(tly.y, tuy.y)), fminf(fmaxf(tlz.y, tuz.y), tlim));
+    const f32x2 n = f32x2{tn0, tn1} * f32x2{LO, LO}, x = f32x2{tx0, tx1} * f32x2{HI, HI};
+    h0 = n.x <= x.x;
+    h1 = n.y <= x.y;
 }
 // Stage the BVH nodes and the sphere rows in this workgroup's LDS (every thread of the block,
 // before any traversal) when the launch placed them there (l_bvh >= 0).
@@ -605,7 +629,7 @@ __device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &
                               : reinterpret_cast<const double2 *>(S.tab + h.o_sph);
     unsigned *stk = reinterpret_cast<unsigned *>(g_lds + h.l_stack) + (threadIdx.x >> 6) * (64 * h.bvh_depth) +
                     (threadIdx.x & 63);
-    const BvhRay ray{(float)o.x, (float)o.y, (float)o.z, bvh_inv(d.x), bvh_inv(d.y), bvh_inv(d.z)};
+    const BvhRay ray = bvh_ray(o, d);
     constexpr float HI = 1.0f + 0x1p-16f;
     float tlim = __builtin_inff();
     // sphere k (local index, compact id id), as sphere_BC<false> + sph_t (the candidate walk's
@@ -629,8 +653,8 @@ __device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &
         RT_STAT(ST_BVH_ITER, 1);
         const float4 a = nodes[node * 4], b = nodes[node * 4 + 1], c = nodes[node * 4 + 2], e = nodes[node * 4 + 3];
         float tn0, tn1;
-        bool h0 = bvh_slab(ray, a.x, a.y, a.z, a.w, b.x, b.y, tlim, tn0);
-        bool h1 = bvh_slab(ray, b.z, b.w, c.x, c.y, c.z, c.w, tlim, tn1);
+        bool h0, h1;
+        bvh_slab2(ray, a, b, c, tlim, h0, tn0, h1, tn1);
         const int c0 = __float_as_int(e.x), c1 = __float_as_int(e.y);
         if (h0 && c0 < 0) {
             leaf(~c0, __float_as_int(e.z));
@@ -1683,7 +1707,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         rhdr.l_stack = (int)lds_bvh;
         lds_bvh += (size_t)BLOCK * rhdr.bvh_depth * sizeof(unsigned);
     }
-    auto lds_r = [&](int k) { return rhdr.bvh_ok && k >= rhdr.bvh_level ? lds_bvh : lds; };
+    auto lds_r = [&](int k) { return !staged && rhdr.bvh_ok && k >= rhdr.bvh_level ? lds_bvh : lds; };
     // no side streams (frames in flight): each level's shading fused into the next reflection
     // pass (k_reflect_shade)
     const bool fuse = fuse_on() && !overlap && !levels && nrefl > 0;
@@ -1754,28 +1778,32 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             // waves each, bound by one wave's dependent chain: they walk two candidates per step
             KtScope kt(p, k == 1 ? RT_KT_LEVEL1 : 0, st);
             if (fuse) {
-#define RT_RS(SPHV, ILPV, LDSV)                                                                                     \
-    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV>), dim3(sblocks), dim3(BLOCK), LDSV, st, rhdr,         \
+#define RT_RS(SPHV, ILPV, LDSV, BVHV)                                                                               \
+    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV>), dim3(sblocks), dim3(BLOCK), LDSV, st, rhdr,   \
                        p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
                        colk(k - 1), litk(k - 1), g)
-                if (staged && k == 1) RT_RS(2, false, lds_r(k));
-                else if (staged) RT_RS(2, true, lds_r(k));
-                else if (sph_only && k == 1) RT_RS(1, false, lds_r(k));
-                else if (sph_only) RT_RS(1, true, lds_r(k));
-                else if (k == 1) RT_RS(0, false, lds_r(k));
-                else RT_RS(0, true, lds_r(k));
+                // levels traversing the sphere BVH (unstaged scenes only): the BVH instantiations
+                const bool bvh_k = !staged && rhdr.bvh_ok && k >= rhdr.bvh_level;
+                if (staged && k == 1) RT_RS(2, false, lds, false);
+                else if (staged) RT_RS(2, true, lds, false);
+                else if (sph_only && bvh_k) RT_RS(1, true, lds_r(k), true);
+                else if (sph_only && k == 1) RT_RS(1, false, lds, false);
+                else if (sph_only) RT_RS(1, true, lds, false);
+                else if (bvh_k) RT_RS(0, true, lds_r(k), true);
+                else if (k == 1) RT_RS(0, false, lds, false);
+                else RT_RS(0, true, lds, false);
 #undef RT_RS
             } else if (lv && k == 1)
-                hipLaunchKernelGGL((k_reflect<true, false>), dim3(sblocks), dim3(BLOCK), lds_r(k), st, rhdr, p->d_tab,
+                hipLaunchKernelGGL((k_reflect<true, false>), dim3(sblocks), dim3(BLOCK), lds, st, rhdr, p->d_tab,
                                    p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             else if (lv)
-                hipLaunchKernelGGL((k_reflect<true, true>), dim3(sblocks), dim3(BLOCK), lds_r(k), st, rhdr, p->d_tab,
+                hipLaunchKernelGGL((k_reflect<true, true>), dim3(sblocks), dim3(BLOCK), lds, st, rhdr, p->d_tab,
                                    p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             else if (k == 1)
-                hipLaunchKernelGGL((k_reflect<false, false>), dim3(sblocks), dim3(BLOCK), lds_r(k), st, rhdr, p->d_tab,
+                hipLaunchKernelGGL((k_reflect<false, false>), dim3(sblocks), dim3(BLOCK), lds, st, rhdr, p->d_tab,
                                    p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             else
-                hipLaunchKernelGGL((k_reflect<false, true>), dim3(sblocks), dim3(BLOCK), lds_r(k), st, rhdr, p->d_tab,
+                hipLaunchKernelGGL((k_reflect<false, true>), dim3(sblocks), dim3(BLOCK), lds, st, rhdr, p->d_tab,
                                    p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
             HIPCHK(hipGetLastError());
             if ((rc = level_lists(k)) != RT_OK) return rc;

@@ -212,10 +212,14 @@ static void build_bvh(const std::vector<rt_elem> &e, const std::vector<int> &sph
     for (const Node &nd : nodes) {
         float f[16];
         const Box &b0 = nd.b[0], &b1 = nd.b[1];
-        f[0] = f32_down(b0.lo[0]); f[1] = f32_down(b0.lo[1]); f[2] = f32_down(b0.lo[2]);
-        f[3] = f32_up(b0.hi[0]); f[4] = f32_up(b0.hi[1]); f[5] = f32_up(b0.hi[2]);
-        f[6] = f32_down(b1.lo[0]); f[7] = f32_down(b1.lo[1]); f[8] = f32_down(b1.lo[2]);
-        f[9] = f32_up(b1.hi[0]); f[10] = f32_up(b1.hi[1]); f[11] = f32_up(b1.hi[2]);
+        // (lx0 lx1 ly0 ly1) (lz0 lz1 ux0 ux1) (uy0 uy1 uz0 uz1): the two children's bounds side by
+        // side, so the kernel's slab distances of both are packed binary32 pairs
+        for (int a = 0; a < 3; ++a) {
+            f[2 * a] = f32_down(b0.lo[a]);
+            f[2 * a + 1] = f32_down(b1.lo[a]);
+            f[6 + 2 * a] = f32_up(b0.hi[a]);
+            f[6 + 2 * a + 1] = f32_up(b1.hi[a]);
+        }
         std::memcpy(&f[12], &nd.ch[0], 4);
         std::memcpy(&f[13], &nd.ch[1], 4);
         const int id0 = nd.ch[0] < 0 ? compact[sph[~nd.ch[0]]] : -1, id1 = nd.ch[1] < 0 ? compact[sph[~nd.ch[1]]] : -1;
