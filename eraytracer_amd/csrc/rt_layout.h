@@ -93,6 +93,7 @@ struct SceneHdr {
     double dz;   // (0 + (0 + (1*F + Lz))) - Lz : z of Through - From
     double screen_w, screen_h;
     double n_light_d; // number of lights as a double (ORDER_FAST weight)
+    double ext;       // largest |coordinate| (+ radius) of the origins and spheres (binary32 culling margins)
 };
 
 } // namespace rtl

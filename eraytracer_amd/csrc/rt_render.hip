@@ -449,6 +449,96 @@ __device__ __forceinline__ unsigned long long cull_chunk(const Scene &S, const B
     return __ballot(in & keep);
 }
 
+// ---- Binary32 beams for reflection rays ------------------------------------------------------
+// The reflection scans' beams (origin ball + direction cone over a group of lanes) and their
+// per-sphere cull tests are filters: they only have to keep every sphere some ray of the group
+// can hit.  They run in binary32 (hardware sqrt / reciprocal, half the issue cost of binary64,
+// single-register DPP reductions) with margins far above binary32 rounding: BEAM32_EPS (1e-5,
+// vs ~1e-6 accumulated relative error in the O(1) cosines and sines), and the positions' rounding
+// (|x| * 2^-24 per coordinate) covered by widening the origin ball by (|origins| + extent) * 1e-6.
+// The axis need not be a unit vector: the cone bounds and the sphere test scale with |axis| alike.
+constexpr float BEAM32_EPS = 1.0e-5f;
+struct Beam32 {
+    float ax, ay, az; // axis (about unit)
+    float c, s;       // lower bound of the lanes' a.d, upper bound of |a x d|
+    float mx, my, mz; // origin ball centre
+    float ro;         // origin ball radius, position rounding included
+    bool on;
+};
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_f32(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+template <typename Op>
+__device__ __forceinline__ float wave_reduce32(float v, Op op) {
+    v = op(v, dpp_f32<DPP_XOR1>(v));
+    v = op(v, dpp_f32<DPP_XOR2>(v));
+    v = op(v, dpp_f32<DPP_HALF_MIRROR>(v));
+    v = op(v, dpp_f32<DPP_MIRROR>(v));
+    return op(op(lane_f32(v, 0), lane_f32(v, 16)), op(lane_f32(v, 32), lane_f32(v, 48)));
+}
+// Must be called with the whole wave converged.  o, d: the lanes' ray origins and directions.
+__device__ __forceinline__ Beam32 make_beam32(const SceneHdr &h, bool act, const D3 &o, const D3 &d) {
+    Beam32 b;
+    b.on = false;
+    b.ax = b.ay = b.az = b.c = b.s = b.mx = b.my = b.mz = b.ro = 0.0f;
+    const unsigned long long am = __ballot(act);
+    if (!h.beam_ok || am == 0) return b;
+    const int al = ((am >> 27) & 1) ? 27 : __builtin_ctzll(am);
+    const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+    const float rx = lane_f32(dx, al), ry = lane_f32(dy, al), rz = lane_f32(dz, al);
+    const float n2 = rx * rx + ry * ry + rz * rz;
+    if (!(n2 > 1.0e-6f)) return b;
+    const float inv = __builtin_amdgcn_rsqf(n2);
+    const float ax = rx * inv, ay = ry * inv, az = rz * inv;
+    // the lanes' directions are unit vectors to ~1e-15 (make_beam); bounds widened by 2 * DIR_TOL
+    constexpr float DIR_TOL = 1.0e-6f;
+    const float dd = dx * dx + dy * dy + dz * dz;
+    const float cl = ax * dx + ay * dy + az * dz;
+    const float qx = ay * dz - az * dy, qy = az * dx - ax * dz, qz = ax * dy - ay * dx;
+    const float sl = __builtin_sqrtf(qx * qx + qy * qy + qz * qz);
+    const bool bad = act && !(dd > 1.0f - 0.5f * DIR_TOL && dd < 1.0f + 0.5f * DIR_TOL);
+    const float c = wave_reduce32(act ? cl : 2.0f, [](float x, float y) { return fminf(x, y); }) - BEAM32_EPS - 2 * DIR_TOL;
+    const float s = wave_reduce32(act ? sl : 0.0f, [](float x, float y) { return fmaxf(x, y); }) + BEAM32_EPS + 2 * DIR_TOL;
+    if (__ballot(bad) != 0 || !(c > 0.0f)) return b; // cone wider than a hemisphere: scan everything
+    const int first = __builtin_ctzll(am);
+    const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+    b.mx = lane_f32(ox, first);
+    b.my = lane_f32(oy, first);
+    b.mz = lane_f32(oz, first);
+    const float ex = ox - b.mx, ey = oy - b.my, ez = oz - b.mz;
+    const float r2 = wave_reduce32(act ? ex * ex + ey * ey + ez * ez : 0.0f, [](float x, float y) { return fmaxf(x, y); });
+    const double mo = wave_max(act ? fmax(fabs(o.x), fmax(fabs(o.y), fabs(o.z))) : 0.0);
+    if (!(mo <= CULL_EXTENT)) return b;
+    b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
+    b.ro = __builtin_sqrtf(r2) * (1.0f + BEAM32_EPS) + BEAM32_EPS + (float)((mo + h.ext) * 1.0e-6);
+    b.on = true;
+    return b;
+}
+// Candidate mask of spheres [chunk, chunk+64) for a binary32 beam (lane j tests sphere chunk+j).
+template <int SPH = 0>
+__device__ __forceinline__ unsigned long long cull_chunk32(const Scene &S, const Beam32 &b, int chunk) {
+    const SceneHdr &h = S.h;
+    const int k = chunk + (int)(threadIdx.x & 63);
+    const bool in = k < h.n_sph;
+    const int kk = in ? k : 0;
+    const double2 *g = SPH == 2 ? reinterpret_cast<const double2 *>(g_lds + h.l_sphb) + kk * (SPH_B_W / 2)
+                                : reinterpret_cast<const double2 *>(S.tab + h.o_sph_b + kk * SPH_B_W);
+    const double2 g01 = g[0], g23 = g[1];
+    const float vx = (float)g01.x - b.mx, vy = (float)g01.y - b.my, vz = (float)g23.x - b.mz;
+    const float vl = __builtin_sqrtf(vx * vx + vy * vy + vz * vz);
+    const float rp = (float)g23.y + b.ro;
+    const float sr = rp * __builtin_amdgcn_rcpf(vl) * (1.0f + BEAM32_EPS) + BEAM32_EPS;
+    const float cr = __builtin_sqrtf(fmaxf(1.0f - sr * sr, 0.0f)) - BEAM32_EPS;
+    const float thr = b.c * cr - b.s * sr;
+    const float av = b.ax * vx + b.ay * vy + b.az * vz;
+    const bool keep = (vl <= rp * (1.0f + BEAM32_EPS) + BEAM32_EPS) | (sr >= 1.0f) | !(av + BEAM32_EPS * vl < thr * vl);
+    return __ballot(in & keep);
+}
+
 __device__ __forceinline__ unsigned long long chunk_all(int n_sph, int chunk) {
     const int n = n_sph - chunk;
     return n >= 64 ? ~0ull : ((1ull << n) - 1);
@@ -722,7 +812,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
             const int gv = __builtin_amdgcn_readlane(grp, __builtin_ctzll(rem));
             const bool sel = (g == MAX_GROUPS - 1) ? ((rem >> (threadIdx.x & 63)) & 1) != 0 : (act && grp == gv);
             rem &= ~__ballot(sel);
-            const Beam b = make_beam(h, sel, o, d, false);
+            const Beam32 b = make_beam32(h, sel, o, d);
             RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
             if (!b.on) {
                 all = true;
@@ -730,7 +820,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
             }
 #pragma unroll
             for (int c = 0; c < UCH; ++c)
-                if (c < nch) m[c] |= cull_chunk<SPH>(S, b, c * 64, -1);
+                if (c < nch) m[c] |= cull_chunk32<SPH>(S, b, c * 64);
         }
 #pragma unroll
         for (int c = 0; c < UCH; ++c)
@@ -744,14 +834,25 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
             sel = (g == MAX_GROUPS - 1) ? ((rem >> (threadIdx.x & 63)) & 1) != 0 : (act && grp == gv);
         }
         rem = PRE ? 0ull : (rem & ~__ballot(sel));
-        const Beam b = make_beam(h, sel, o, d, PRE);
-        RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
-        for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
-            const unsigned long long m =
-                b.on ? cull_chunk<SPH>(S, b, chunk, PRE ? org : -1) : chunk_all(h.n_sph, chunk);
-            scan_spheres<PRE, ILP>(S, org, o, d, A4, chunk, m, bt, bid);
+        bool on;
+        if constexpr (PRE) {
+            const Beam b = make_beam(h, sel, o, d, true);
+            on = b.on;
+            RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
+            for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
+                const unsigned long long m = b.on ? cull_chunk<SPH>(S, b, chunk, org) : chunk_all(h.n_sph, chunk);
+                scan_spheres<PRE, ILP>(S, org, o, d, A4, chunk, m, bt, bid);
+            }
+        } else {
+            const Beam32 b = make_beam32(h, sel, o, d);
+            on = b.on;
+            RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
+            for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
+                const unsigned long long m = b.on ? cull_chunk32<SPH>(S, b, chunk) : chunk_all(h.n_sph, chunk);
+                scan_spheres<PRE, ILP>(S, org, o, d, A4, chunk, m, bt, bid);
+            }
         }
-        if (!b.on) break; // everything was scanned
+        if (!on) break; // everything was scanned
     }
     scan_tri_pl<PRE>(S, org, o, d, bt, bid);
     return (act && bid != 0x7fffffff) ? bid : -1;

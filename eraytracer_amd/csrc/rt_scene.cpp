@@ -398,6 +398,7 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
             grow(s.center.x); grow(s.center.y); grow(s.center.z); grow(s.radius);
         }
         h.cull_ok = ext <= CULL_EXTENT ? 1 : 0;
+        h.ext = ext;
     }
     // Wave beams (a cone over the wave's rays, a candidate mask per 64 spheres) cost a few wave
     // reductions per scan; with a handful of spheres testing every one is cheaper
