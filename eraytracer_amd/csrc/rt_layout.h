@@ -34,6 +34,9 @@ constexpr int SPH_B_W = 4;   // cx cy cz r
 constexpr int SPH_OB_W = 8;  // vx vy vz (= c - o), |v|, sin(rho) upper bound, cos(rho) lower bound, near(0/1),
                              // lower bound of |v| - r (no ray from o reaches the sphere before that distance)
 
+constexpr int SPH_OB32_W = 8; // floats
+constexpr float BEAM32_EPS = 1.0e-5f; // binary32 beams' margin (rt_render.hip, "Binary32 beams")
+
 // Culling is exact only while every binary64 rounding error in the reference's sphere test is
 // far below its 0.001 discriminant threshold: all scene coordinates within this bound.
 constexpr double CULL_EXTENT = 1.0e4;
@@ -68,6 +71,9 @@ struct SceneHdr {
     int int_pow;                                   // every specular power is an integer in [0, 1024]
     // offsets into tab
     int o_sph, o_sph_org, o_tri, o_tri_org, o_pl, o_pl_org, o_obj, o_light, o_sph_b, o_sph_ob;
+    // binary32 copy of the per-origin cone rows for the binary32 beams (SPH_OB32_W floats per row:
+    // v (3), |v|, sin(rho) and cos(rho) bounds with BEAM32 margins, near, |v| - r lower bound)
+    int o_sph_ob32;
     // offsets into itab
     int i_sph_id, i_tri_id, i_pl_id, i_obj_meta;
     // Occluder masks (only when cull_ok): for light i, target sphere t and 64-sphere chunk k,

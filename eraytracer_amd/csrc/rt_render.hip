@@ -457,7 +457,6 @@ __device__ __forceinline__ unsigned long long cull_chunk(const Scene &S, const B
 // vs ~1e-6 accumulated relative error in the O(1) cosines and sines), and the positions' rounding
 // (|x| * 2^-24 per coordinate) covered by widening the origin ball by (|origins| + extent) * 1e-6.
 // The axis need not be a unit vector: the cone bounds and the sphere test scale with |axis| alike.
-constexpr float BEAM32_EPS = 1.0e-5f;
 struct Beam32 {
     float ax, ay, az; // axis (about unit)
     float c, s;       // lower bound of the lanes' a.d, upper bound of |a x d|
@@ -537,6 +536,69 @@ __device__ __forceinline__ unsigned long long cull_chunk32(const Scene &S, const
     const float av = b.ax * vx + b.ay * vy + b.az * vz;
     const bool keep = (vl <= rp * (1.0f + BEAM32_EPS) + BEAM32_EPS) | (sr >= 1.0f) | !(av + BEAM32_EPS * vl < thr * vl);
     return __ballot(in & keep);
+}
+
+// Tabled origin `org` (camera, lights): the host's binary32 cone rows (SPH_OB32_W); a sphere whose
+// nearest surface point is farther than tmax from the origin is dropped too.
+__device__ __forceinline__ unsigned long long cull_chunk32_org(const Scene &S, const Beam32 &b, int chunk, int org,
+                                                               float tmax = __builtin_inff()) {
+    const SceneHdr &h = S.h;
+    const int k = chunk + (int)(threadIdx.x & 63);
+    const bool in = k < h.n_sph;
+    const int kk = in ? k : 0;
+    const float4 *q = reinterpret_cast<const float4 *>(S.tab + h.o_sph_ob32) + (size_t)(org * h.n_sph + kk) * 2;
+    const float4 v = q[0], w = q[1]; // (vx vy vz |v|) (sin, cos, near, dlow)
+    const float thr = b.c * w.y - b.s * w.x;
+    const float av = b.ax * v.x + b.ay * v.y + b.az * v.z;
+    const bool keep = ((w.z != 0.0f) | !(av + BEAM32_EPS * v.w < thr * v.w)) & !(w.w > tmax);
+    return __ballot(in & keep);
+}
+
+// Beam of a wave holding two primary rays per lane (an 8x16 pixel block) from a tabled origin:
+// make_beam32's cone over both ray sets (no origin ball).
+__device__ __forceinline__ Beam32 make_beam_pair32(const SceneHdr &h, bool a0, const D3 &d0, bool a1, const D3 &d1) {
+    Beam32 b;
+    b.on = false;
+    b.ax = b.ay = b.az = b.c = b.s = b.mx = b.my = b.mz = b.ro = 0.0f;
+    const unsigned long long m0 = __ballot(a0), m1 = __ballot(a1);
+    if (!h.beam_ok || (m0 | m1) == 0) return b;
+    const float x0 = (float)d0.x, y0 = (float)d0.y, z0 = (float)d0.z;
+    const float x1 = (float)d1.x, y1 = (float)d1.y, z1 = (float)d1.z;
+    // axis: the ray of pixel (3, 7) of the block (set 0, lane 59), else the first active ray
+    float rx, ry, rz;
+    if ((m0 >> 59) & 1) {
+        rx = lane_f32(x0, 59); ry = lane_f32(y0, 59); rz = lane_f32(z0, 59);
+    } else if (m0) {
+        const int l = __builtin_ctzll(m0);
+        rx = lane_f32(x0, l); ry = lane_f32(y0, l); rz = lane_f32(z0, l);
+    } else {
+        const int l = __builtin_ctzll(m1);
+        rx = lane_f32(x1, l); ry = lane_f32(y1, l); rz = lane_f32(z1, l);
+    }
+    const float n2 = rx * rx + ry * ry + rz * rz;
+    if (!(n2 > 1.0e-6f)) return b;
+    const float inv = __builtin_amdgcn_rsqf(n2);
+    const float ax = rx * inv, ay = ry * inv, az = rz * inv;
+    constexpr float DIR_TOL = 1.0e-6f; // as in make_beam32
+    auto lane_terms = [&](bool a, float dx, float dy, float dz, float &cl, float &q2) {
+        const float dd = dx * dx + dy * dy + dz * dz;
+        cl = ax * dx + ay * dy + az * dz;
+        const float qx = ay * dz - az * dy, qy = az * dx - ax * dz, qz = ax * dy - ay * dx;
+        q2 = qx * qx + qy * qy + qz * qz;
+        return a && !(dd > 1.0f - 0.5f * DIR_TOL && dd < 1.0f + 0.5f * DIR_TOL);
+    };
+    float cl0, q20, cl1, q21;
+    const bool bad0 = lane_terms(a0, x0, y0, z0, cl0, q20); // both sets evaluated (no short circuit)
+    const bool bad1 = lane_terms(a1, x1, y1, z1, cl1, q21);
+    const float cmin = fminf(a0 ? cl0 : 2.0f, a1 ? cl1 : 2.0f);
+    const float q2max = fmaxf(a0 ? q20 : 0.0f, a1 ? q21 : 0.0f);
+    const float c = wave_reduce32(cmin, [](float x, float y) { return fminf(x, y); }) - BEAM32_EPS - 2 * DIR_TOL;
+    const float s = __builtin_sqrtf(wave_reduce32(q2max, [](float x, float y) { return fmaxf(x, y); })) * (1.0f + BEAM32_EPS) +
+                    BEAM32_EPS + 2 * DIR_TOL;
+    if (__ballot(bad0 || bad1) != 0 || !(c > 0.0f)) return b;
+    b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
+    b.on = true;
+    return b;
 }
 
 __device__ __forceinline__ unsigned long long chunk_all(int n_sph, int chunk) {
@@ -858,52 +920,6 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
     return (act && bid != 0x7fffffff) ? bid : -1;
 }
 
-// Beam of a wave holding two primary rays per lane (an 8x16 pixel block) from a tabled
-// origin: the same cone construction as make_beam, over both ray sets.
-__device__ __forceinline__ Beam make_beam_pair(const SceneHdr &h, bool a0, const D3 &d0, bool a1, const D3 &d1) {
-    Beam b;
-    b.on = false;
-    b.ax = b.ay = b.az = b.c = b.s = b.mx = b.my = b.mz = b.ro = 0.0;
-    const unsigned long long m0 = __ballot(a0), m1 = __ballot(a1);
-    if (!h.beam_ok || (m0 | m1) == 0) return b;
-    // axis: the ray of pixel (3, 7) of the block (set 0, lane 59), else the first active ray
-    double rx, ry, rz;
-    if ((m0 >> 59) & 1) {
-        rx = lane_f64(d0.x, 59); ry = lane_f64(d0.y, 59); rz = lane_f64(d0.z, 59);
-    } else if (m0) {
-        const int l = __builtin_ctzll(m0);
-        rx = lane_f64(d0.x, l); ry = lane_f64(d0.y, l); rz = lane_f64(d0.z, l);
-    } else {
-        const int l = __builtin_ctzll(m1);
-        rx = lane_f64(d1.x, l); ry = lane_f64(d1.y, l); rz = lane_f64(d1.z, l);
-    }
-    const double n2 = rx * rx + ry * ry + rz * rz;
-    if (!(n2 > 0.0)) return b;
-    const double inv = uniform(1.0 / sqrt(n2));
-    const double ax = rx * inv, ay = ry * inv, az = rz * inv;
-    constexpr double DIR_TOL = 1.0e-6; // as in make_beam
-    auto lane_terms = [&](bool a, const D3 &d, double &cl, double &q2) {
-        const double dd = d.x * d.x + d.y * d.y + d.z * d.z;
-        cl = ax * d.x + ay * d.y + az * d.z;
-        const double qx = ay * d.z - az * d.y, qy = az * d.x - ax * d.z, qz = ax * d.y - ay * d.x;
-        q2 = qx * qx + qy * qy + qz * qz;
-        return a && !(dd > 1.0 - DIR_TOL && dd < 1.0 + DIR_TOL);
-    };
-    double cl0, q20, cl1, q21;
-    const bool bad0 = lane_terms(a0, d0, cl0, q20); // both sets evaluated (no short circuit)
-    const bool bad1 = lane_terms(a1, d1, cl1, q21);
-    const bool bad = bad0 || bad1;
-    const double cmin = fmin(a0 ? cl0 : 2.0, a1 ? cl1 : 2.0);
-    const double q2max = fmax(a0 ? q20 : 0.0, a1 ? q21 : 0.0);
-    const double c = uniform(wave_min(cmin)) - CULL_EPS - 2 * DIR_TOL;
-    // sqrt is monotone and correctly rounded: sqrt(max q2) = max sqrt(q2)
-    const double s = uniform(sqrt(wave_max(q2max))) + CULL_EPS + 2 * DIR_TOL;
-    if (__ballot(bad) != 0 || !(c > 0.0)) return b;
-    b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
-    b.on = true;
-    return b;
-}
-
 // nearest_object_intersecting_ray/6 for two rays per lane from tabled origin `org` (primary
 // rays): one beam and one candidate walk serve both, and each candidate's two tests are
 // independent (instruction-level parallelism for the wave).
@@ -917,10 +933,10 @@ __device__ __forceinline__ void nearest_pair(const Scene &S, int org, const D3 &
     if (__ballot(a0 | a1) == 0) return;
     const double A40 = 4 * (d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
     const double A41 = 4 * (d1.x * d1.x + d1.y * d1.y + d1.z * d1.z);
-    const Beam b = make_beam_pair(h, a0, d0, a1, d1);
+    const Beam32 b = make_beam_pair32(h, a0, d0, a1, d1);
     RT_STAT(ST_NEAR_PRE, 1);
     for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
-        unsigned long long m = b.on ? cull_chunk(S, b, chunk, org) : chunk_all(h.n_sph, chunk);
+        unsigned long long m = b.on ? cull_chunk32_org(S, b, chunk, org) : chunk_all(h.n_sph, chunk);
         RT_STAT(ST_NEAR_PRE_CAND, __popcll(m));
         while (m) {
             const int k = chunk + __builtin_ctzll(m);

@@ -389,6 +389,28 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
             t.insert(t.end(), {vx, vy, vz, vl, sr, cr, near, dlow});
         }
     }
+    // the same rows in binary32 for the binary32 beams: sin(rho) rounded up and widened, cos(rho)
+    // rounded down and narrowed by BEAM32_EPS, |v| - r rounded down
+    h.o_sph_ob32 = (int)t.size();
+    for (const rt_vec3 &o : org) {
+        for (int i : sph) {
+            const auto &s = e[i].u.sphere;
+            double vx = s.center.x - o.x, vy = s.center.y - o.y, vz = s.center.z - o.z;
+            double vl = std::sqrt(vx * vx + vy * vy + vz * vz);
+            double r = std::fabs(s.radius);
+            const double eps = BEAM32_EPS;
+            bool near = vl <= r * (1 + eps) + eps;
+            double sr = near ? 1.0 : r / vl * (1 + eps) + eps;
+            if (sr >= 1.0) near = true;
+            double cr = near ? 0.0 : std::sqrt(1 - sr * sr) - eps;
+            const double dlow = (vl - r) - eps * (vl + r) - eps;
+            float f[SPH_OB32_W] = {(float)vx, (float)vy, (float)vz, (float)vl, f32_up(sr), f32_down(cr),
+                                   near ? 1.0f : 0.0f, f32_down(dlow)};
+            double d[SPH_OB32_W / 2];
+            std::memcpy(d, f, sizeof(d));
+            t.insert(t.end(), d, d + SPH_OB32_W / 2);
+        }
+    }
     {
         double ext = 0;
         auto grow = [&](double v) { ext = std::fmax(ext, std::fabs(v)); };
