@@ -321,6 +321,12 @@ def main():
                 ach = f64 * 64 / (dom_ms / 1e3) / 1e12
                 roof.update(achieved=round(ach, 3), frac=round(ach / PEAK_FP64_VALU_TOPS, 4),
                             f64_wave_insts_per_launch=round(f64))
+                # all VALU issue (binary64 4 cycles per wave instruction, binary32 / integer 2) over the
+                # 1024 SIMDs' cycles: the binding roofline once the filters run in binary32
+                valu = kd.get("counters", {}).get("SQ_INSTS_VALU")
+                if valu:
+                    roof["valu_issue_frac"] = round((4 * f64 + 2 * (valu - f64)) / (1024 * 2.4e9 * dom_ms / 1e3), 4)
+                    roof["valu_wave_insts_per_launch"] = round(valu)
             kc = kd.get("counters", {})
             if "FETCH_SIZE" in kc and "WRITE_SIZE" in kc:  # KiB; FETCH x2 on gfx950 (MI355X_MICROARCH.md)
                 roof["traffic"] = round((2 * kc["FETCH_SIZE"] + kc["WRITE_SIZE"]) * 1024)
@@ -346,7 +352,10 @@ def main():
                         f"on its stream over {args.iso} frames launched back to back after the timed region (in "
                         f"the timed region {inflight} frames in flight share the GPU and a launch's events also "
                         "span its queueing: launch_span_ms_in_flight); launch_ms_rocprof = rocprofv3's average "
-                        "duration of the same launches; traffic = that kernel's HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE). frame_f64_issue_frac / frame_valu_busy_frac: "
+                        "duration of the same launches; traffic = that kernel's HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE). "
+                        "valu_issue_frac: the same kernel's VALU issue cycles (FP64 wave-instructions x 4, other VALU x 2) / "
+                        "(1024 SIMDs x 2.4 GHz x launch time) - the beam and BVH filters run in binary32, so the FP64 fraction "
+                        "alone understates how busy the VALU is. frame_f64_issue_frac / frame_valu_busy_frac: "
                         "all of a frame's kernels over the GPU time per frame. ref_work_tops: the reference's "
                         "brute-force binary64 op count per frame (SURVEY.md 8d) / GPU time per frame, in T op/s "
                         "(culling skips most of it: not a roofline)")
