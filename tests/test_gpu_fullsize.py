@@ -164,3 +164,69 @@ print('fused ok')
     env = dict(os.environ, RT_ENGINE="wave", PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "fused ok" in r.stdout, r.stdout + r.stderr
+
+
+_FUSED_FRAME = r"""
+import ctypes, numpy as np, torch
+from eraytracer_amd import _native as N, scenes
+from oracle import oracle as O
+L = N.lib()
+def frame(sc, w, h, d, side, spp=1, seed=0, shard=0, nshards=1):
+    el = N.marshal(sc)
+    p = ctypes.c_void_p()
+    N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(p)))
+    try:
+        N.check(L.rt_configure(p, N.RT_CFG_SIDE_STREAMS, side))
+        rows = L.rt_shard_rows(h, 16, nshards)
+        img = torch.full((rows, w, 3), float('nan'), dtype=torch.float64, device='cuda')
+        N.check(L.rt_launch_spp(p, w, h, d, 16, shard, nshards, N.RT_OUT_F64, N.RT_ORDER_EXACT, spp, seed,
+                                img.data_ptr(), None, torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        return img.cpu().numpy()
+    finally:
+        L.rt_release(p)
+"""
+
+
+def _child(code, **env):
+    e = dict(os.environ, PYTHONPATH=ROOT, **env)
+    r = subprocess.run([sys.executable, "-c", _FUSED_FRAME + code], cwd=ROOT, env=e, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0 and "ok" in r.stdout.split(), r.stdout + r.stderr
+
+
+def test_bvh_forced_on_every_level_and_scene():
+    """The per-lane sphere BVH (k_reflect_shade<..., BVH>) forced onto every reflection level of
+    scenes it is not chosen for (RT_BVH_MIN=2, RT_BVH_LEVEL=1, read once per process: a child):
+    spheres-only S16/S64/S256 and the mixed scene (BVH spheres + scanned triangles and planes).
+    Each frame equals the side-stream path (beams only) bit for bit and the oracle within 1e-5."""
+    _child(r"""
+for name, w, h, d in [('s16', 80, 64, 5), ('s64', 96, 96, 5), ('s256', 64, 48, 8), ('mixed', 128, 96, 5)]:
+    sc = scenes.named(name)
+    a, b = frame(sc, w, h, d, 1), frame(sc, w, h, d, 0)
+    assert np.array_equal(a.view(np.int64), b.view(np.int64)), name
+    ref = O.render(N.marshal(sc), w, h, d, mode=O.MEMO)
+    assert np.abs(b - ref).max() <= 1e-5, name
+print('ok')
+""", RT_ENGINE="wave", RT_BVH_MIN="2", RT_BVH_LEVEL="1")
+
+
+def test_config5_rows_through_the_bvh_path(oracle):
+    """Config 5 as the bench renders it (frames in flight: no side streams, so levels >= 2 of
+    S256 traverse the BVH): S256 4096x4096 depth 8 x16 spp, 2 of 8 interleaved row shards, bit for
+    bit the side-stream path's (beams only) and 3 rows of each against the oracle."""
+    _child(r"""
+sc = scenes.s256()
+W = H = 4096
+seed = 0x5EED0005
+el = N.marshal(sc)
+for shard in (0, 5):
+    a = frame(sc, W, H, 8, 1, 16, seed, shard, 8)
+    b = frame(sc, W, H, 8, 0, 16, seed, shard, 8)
+    assert np.array_equal(a.view(np.int64), b.view(np.int64)), shard
+    for lr in (0, 200, 511):
+        gy = (lr // 16 * 8 + shard) * 16 + lr % 16
+        ref = O.render(el, W, H, 8, mode=O.MEMO, row0=gy, nrows=1, spp=16, seed=seed)
+        assert np.abs(b[lr:lr + 1] - ref).max() <= 1e-5, (shard, lr)
+print('ok')
+""")
