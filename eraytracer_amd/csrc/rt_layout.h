@@ -49,7 +49,7 @@ constexpr int OBJ_META_W = 4; // kind, local index within its type, canon compac
 constexpr int LDS_STAGE_MAX = 32 * 1024; // 5 workgroups per CU keep their 32 KiB each
 
 // Sphere BVH for incoherent reflection rays (see rt_render.hip, "Per-lane BVH"): a binary tree
-// over the spheres, built on the host by median splits (depth = ceil(log2 n_sph)); one 64-byte
+// over the spheres, built on the host by SAH splits (depth <= ceil(log2 n_sph) + 2); one 64-byte
 // node holds both children's binary32 boxes (rounded outwards and inflated, so the box test
 // never rejects a sphere the binary64 test accepts), their links (>= 0: node, < 0: ~sphere) and,
 // for a sphere child, the sphere's compact object id.
@@ -58,6 +58,7 @@ constexpr int BVH_LDS_MAX = 40 * 1024; // nodes + sphere rows staged in LDS up t
 constexpr int BVH_STACK = 12;        // per-lane traversal stack entries (tree depth <= BVH_STACK: 4096 spheres)
 constexpr int BVH_MIN_SPHERES = 128; // below this the wave beams are cheaper (default; RT_BVH_MIN)
 constexpr int BVH_LEVEL = 2;         // first reflection level traversing the BVH (default; RT_BVH_LEVEL)
+constexpr int BVH_SAH_SLACK = 2;     // SAH trees may be this much deeper than ceil(log2 n_sph) (RT_BVH_SAH_SLACK)
 constexpr double BVH_BOX_REL = 1.0e-5; // box inflation, relative to the scene extent (+1)
 
 enum ObjKind : int { K_SPHERE = 0, K_TRIANGLE = 1, K_PLANE = 2 };

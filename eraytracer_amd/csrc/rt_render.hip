@@ -765,20 +765,23 @@ __device__ __forceinline__ void stage_bvh(const Scene &S) {
     const int4 *sn = reinterpret_cast<const int4 *>(S.tab + h.o_bvh);
     int4 *dn = reinterpret_cast<int4 *>(g_lds + h.l_bvh);
     for (int i = threadIdx.x; i < h.n_bvh * 4; i += blockDim.x) dn[i] = sn[i];
-    const int4 *ss = reinterpret_cast<const int4 *>(S.tab + h.o_sph);
-    int4 *ds = reinterpret_cast<int4 *>(g_lds + h.l_bsph);
-    for (int i = threadIdx.x; i < h.n_sph * 2; i += blockDim.x) ds[i] = ss[i];
+    if (h.l_bsph >= 0) {
+        const int4 *ss = reinterpret_cast<const int4 *>(S.tab + h.o_sph);
+        int4 *ds = reinterpret_cast<int4 *>(g_lds + h.l_bsph);
+        for (int i = threadIdx.x; i < h.n_sph * 2; i += blockDim.x) ds[i] = ss[i];
+    }
     __syncthreads();
 }
-// LDS: the nodes and sphere rows are staged in LDS (h.l_bvh >= 0), else read from HBM (L2)
-template <bool LDS>
+// LDS: the nodes are staged in LDS (h.l_bvh >= 0), ROWS: the sphere rows too (h.l_bsph >= 0);
+// else read from HBM (L2)
+template <bool LDS, bool ROWS>
 __device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &d, double A4, bool act, double &bt,
                                          int &bid) {
     const SceneHdr &h = S.h;
     const float4 *nodes = LDS ? reinterpret_cast<const float4 *>(g_lds + h.l_bvh)
                               : reinterpret_cast<const float4 *>(S.tab + h.o_bvh);
-    const double2 *rows = LDS ? reinterpret_cast<const double2 *>(g_lds + h.l_bsph)
-                              : reinterpret_cast<const double2 *>(S.tab + h.o_sph);
+    const double2 *rows = ROWS ? reinterpret_cast<const double2 *>(g_lds + h.l_bsph)
+                               : reinterpret_cast<const double2 *>(S.tab + h.o_sph);
     unsigned *stk = reinterpret_cast<unsigned *>(g_lds + h.l_stack) + (threadIdx.x >> 6) * (64 * h.bvh_depth) +
                     (threadIdx.x & 63);
     const BvhRay ray = bvh_ray(o, d);
@@ -853,10 +856,12 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
     RT_STAT(PRE ? ST_NEAR_PRE : ST_NEAR_GEN, 1);
     RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
     if (!PRE && bvh) { // (wave-uniform) per-lane BVH traversal, then the triangles and planes
-        if (h.l_bvh >= 0)
-            scan_bvh<true>(S, o, d, A4, act, bt, bid);
+        if (h.l_bvh >= 0 && h.l_bsph >= 0)
+            scan_bvh<true, true>(S, o, d, A4, act, bt, bid);
+        else if (h.l_bvh >= 0)
+            scan_bvh<true, false>(S, o, d, A4, act, bt, bid);
         else
-            scan_bvh<false>(S, o, d, A4, act, bt, bid);
+            scan_bvh<false, false>(S, o, d, A4, act, bt, bid);
         scan_tri_pl<PRE>(S, org, o, d, bt, bid);
         return (act && bid != 0x7fffffff) ? bid : -1;
     }
@@ -1815,10 +1820,16 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     SceneHdr rhdr = p->hdr;
     size_t lds_bvh = lds;
     if (rhdr.bvh_ok) {
-        const size_t nb = (size_t)rhdr.n_bvh * BVH_NODE_DOUBLES * 8, sb = (size_t)rhdr.n_sph * SPH_W * 8;
+        // RT_BVH_ROWS_LDS=0: the sphere rows stay in HBM (L1/L2 hits), leaving LDS to the nodes and
+        // a deeper stack (A/B)
+        static const bool rows_lds = [] {
+            const char *e = std::getenv("RT_BVH_ROWS_LDS");
+            return !(e && std::strcmp(e, "0") == 0);
+        }();
+        const size_t nb = (size_t)rhdr.n_bvh * BVH_NODE_DOUBLES * 8, sb = rows_lds ? (size_t)rhdr.n_sph * SPH_W * 8 : 0;
         if (nb + sb <= (size_t)BVH_LDS_MAX) {
             rhdr.l_bvh = (int)lds_bvh;
-            rhdr.l_bsph = (int)(lds_bvh + nb);
+            rhdr.l_bsph = rows_lds ? (int)(lds_bvh + nb) : -1;
             lds_bvh += nb + sb;
         }
         rhdr.l_stack = (int)lds_bvh;
