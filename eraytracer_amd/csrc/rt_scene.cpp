@@ -317,6 +317,21 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
         else if (e[i].kind == RT_TRIANGLE) tri.push_back(i);
         else pl.push_back(i);
     }
+    // The spheres' table order (their local index) decides only the order candidates and occluders
+    // are visited in — nearest hits are broken by list position (compact id), shadow answers are
+    // any-hit — so in scenes with long occluder walks (more than 64 spheres) larger spheres go
+    // first: a shadow ray meets the likelier blockers early and its lane leaves sooner (measured:
+    // config 5 -3 %; S64, 1.4 occluder steps per test, is 1 % faster in list order).
+    // RT_SPH_ORDER=list | radius forces one, for A/B.
+    static const int order = [] {
+        const char *s = std::getenv("RT_SPH_ORDER");
+        return !s ? 0 : std::strcmp(s, "list") == 0 ? 1 : std::strcmp(s, "radius") == 0 ? 2 : 0;
+    }();
+    const bool by_radius = order == 2 || (order == 0 && sph.size() > 64);
+    if (by_radius)
+        std::stable_sort(sph.begin(), sph.end(), [&](int a, int b) {
+            return std::fabs(e[a].u.sphere.radius) > std::fabs(e[b].u.sphere.radius);
+        });
 
     SceneHdr &h = out.hdr;
     std::memset(&h, 0, sizeof(h));
