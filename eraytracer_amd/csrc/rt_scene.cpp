@@ -319,19 +319,32 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
     }
     // The spheres' table order (their local index) decides only the order candidates and occluders
     // are visited in — nearest hits are broken by list position (compact id), shadow answers are
-    // any-hit — so in scenes with long occluder walks (more than 64 spheres) larger spheres go
-    // first: a shadow ray meets the likelier blockers early and its lane leaves sooner (measured:
-    // config 5 -3 %; S64, 1.4 occluder steps per test, is 1 % faster in list order).
-    // RT_SPH_ORDER=list | radius forces one, for A/B.
+    // any-hit — so in scenes with long occluder walks (more than 64 spheres) the spheres that
+    // cover most of the lights' view go first: a shadow ray meets the likelier blockers early and
+    // its lane leaves sooner (measured, config 5: -3 % ordered by radius, -4.5 % by the solid
+    // angle summed over the lights; S64, 1.4 occluder steps per test, is 1 % faster in list order).
+    // RT_SPH_ORDER=list | radius (the solid-angle order) forces one, for A/B.
     static const int order = [] {
         const char *s = std::getenv("RT_SPH_ORDER");
         return !s ? 0 : std::strcmp(s, "list") == 0 ? 1 : std::strcmp(s, "radius") == 0 ? 2 : 0;
     }();
     const bool by_radius = order == 2 || (order == 0 && sph.size() > 64);
-    if (by_radius)
-        std::stable_sort(sph.begin(), sph.end(), [&](int a, int b) {
-            return std::fabs(e[a].u.sphere.radius) > std::fabs(e[b].u.sphere.radius);
-        });
+    if (by_radius) {
+        // the spheres' solid angle summed over the lights (their radius when there are none)
+        std::vector<double> w(e.size(), 0.0);
+        for (int i : sph) {
+            const auto &sp = e[i].u.sphere;
+            const double r2 = sp.radius * sp.radius;
+            double a = lights.empty() ? r2 : 0.0;
+            for (int li : lights) {
+                const rt_vec3 &L = e[li].u.point_light.location;
+                const double dx = sp.center.x - L.x, dy = sp.center.y - L.y, dz = sp.center.z - L.z;
+                a += r2 / std::fmax(dx * dx + dy * dy + dz * dz, 1e-300);
+            }
+            w[i] = a;
+        }
+        std::stable_sort(sph.begin(), sph.end(), [&](int a, int b) { return w[a] > w[b]; });
+    }
 
     SceneHdr &h = out.hdr;
     std::memset(&h, 0, sizeof(h));
