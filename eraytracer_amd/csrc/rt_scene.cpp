@@ -319,16 +319,15 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
     }
     // The spheres' table order (their local index) decides only the order candidates and occluders
     // are visited in — nearest hits are broken by list position (compact id), shadow answers are
-    // any-hit — so in scenes with long occluder walks (more than 64 spheres) the spheres that
-    // cover most of the lights' view go first: a shadow ray meets the likelier blockers early and
-    // its lane leaves sooner (measured, config 5: -3 % ordered by radius, -4.5 % by the solid
-    // angle summed over the lights; S64, 1.4 occluder steps per test, is 1 % faster in list order).
-    // RT_SPH_ORDER=list | radius (the solid-angle order) forces one, for A/B.
+    // any-hit — so the spheres that cover most of the lights' view go first: a shadow ray's
+    // occluder walk meets the likelier blockers early and its lane leaves sooner (measured against
+    // list order: config 5 -4.5 % per frame, config 3 -1 %; ordering by radius alone: -3 %, and +1 %
+    // on config 3).  RT_SPH_ORDER=list keeps the list order, for A/B.
     static const int order = [] {
         const char *s = std::getenv("RT_SPH_ORDER");
         return !s ? 0 : std::strcmp(s, "list") == 0 ? 1 : std::strcmp(s, "radius") == 0 ? 2 : 0;
     }();
-    const bool by_radius = order == 2 || (order == 0 && sph.size() > 64);
+    const bool by_radius = order != 1;
     if (by_radius) {
         // the spheres' solid angle summed over the lights (their radius when there are none)
         std::vector<double> w(e.size(), 0.0);
