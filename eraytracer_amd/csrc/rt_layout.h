@@ -46,6 +46,15 @@ constexpr int BEAM_MIN_SPHERES = 8;  // fewer spheres: scans test every sphere (
 // int-table record widths (ints)
 constexpr int OBJ_META_W = 4; // kind, local index within its type, canon compact id, canon's local index
 
+// Shadow rays from a light into the cone around a target sphere are split into OCC_CELLS
+// direction cells (occ_cell); each cell has its own, smaller, occluder mask.
+#ifndef RT_OCC_CELLS
+#define RT_OCC_CELLS 4 // 1: one mask per (light, target), as before the cells
+#endif
+constexpr int OCC_CELLS = RT_OCC_CELLS;
+constexpr float OCC_CELL_EPS = 1.0e-4f; // cells overlap by this much (unit-vector components)
+constexpr int OCC_CELLS_MIN_SPHERES = 128; // smaller scenes keep one cell
+
 constexpr int LDS_STAGE_MAX = 32 * 1024; // 5 workgroups per CU keep their 32 KiB each
 
 // Sphere BVH for incoherent reflection rays (see rt_render.hip, "Per-lane BVH"): a binary tree
@@ -77,10 +86,12 @@ struct SceneHdr {
     int o_sph_ob32;
     // offsets into itab
     int i_sph_id, i_tri_id, i_pl_id, i_obj_meta;
-    // Occluder masks (only when cull_ok): for light i, target sphere t and 64-sphere chunk k,
-    // the uint64 at itab[i_occ + 2*((i*n_sph + t)*n_chunk + k)] has bit j set iff sphere
-    // 64k+j can block a shadow ray from light i to any point of sphere t (see rt_scene.cpp).
-    int i_occ, n_chunk;
+    // Occluder masks (only when cull_ok): for light i, target sphere t, direction cell e
+    // (occ_cell; occ_cells of them: OCC_CELLS for scenes whose tables stay in L2, 1 for scenes
+    // staged in LDS) and 64-sphere chunk k, the uint64 at
+    // itab[i_occ + 2*(((i*n_sph + t)*occ_cells + e)*n_chunk + k)] has bit j set iff sphere 64k+j
+    // can block a shadow ray from light i into cell e of the cone towards sphere t (rt_scene.cpp).
+    int i_occ, n_chunk, occ_cells;
     // LDS staging (spheres-only scenes with culling whose per-lane-gathered tables fit
     // LDS_STAGE_MAX bytes; l_bytes = 0 otherwise): byte offsets in the workgroup's dynamic LDS of
     // the object rows (o_obj), object meta rows (i_obj_meta), the lights' per-origin sphere rows

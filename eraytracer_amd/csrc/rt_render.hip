@@ -256,10 +256,11 @@ __device__ __forceinline__ const double *org_row(const Scene &S, int org, int k)
     if (SPH == 2) return reinterpret_cast<const double *>(g_lds + S.h.l_org) + ((org - 1) * S.h.n_sph + k) * SPH_ORG_W;
     return S.tab + S.h.o_sph_org + (org * S.h.n_sph + k) * SPH_ORG_W;
 }
-// occluder masks of `light`, chunk `chunk64`: element t*n_chunk is target sphere t's mask
+// occluder masks of `light`, chunk `chunk64`: element (t*OCC_CELLS + e)*n_chunk is the mask of
+// target sphere t, direction cell e
 template <int SPH>
 __device__ __forceinline__ const unsigned long long *occ_masks(const Scene &S, int light, int chunk64) {
-    const int w = (light * S.h.n_sph) * S.h.n_chunk + chunk64;
+    const int w = (light * S.h.n_sph * (SPH == 2 ? 1 : S.h.occ_cells)) * S.h.n_chunk + chunk64; // staged: 1 cell
     if (SPH == 2) return reinterpret_cast<const unsigned long long *>(g_lds + S.h.l_occ) + w;
     return reinterpret_cast<const unsigned long long *>(S.itab + S.h.i_occ) + w;
 }
@@ -285,7 +286,7 @@ __device__ __forceinline__ void stage_tables(const Scene &S) {
     copy16(h.l_obj, S.tab + h.o_obj, h.n_obj * OBJ_W * 8);
     copy16(h.l_meta, S.itab + h.i_obj_meta, h.n_obj * OBJ_META_W * 4);
     copy16(h.l_org, S.tab + h.o_sph_org + h.n_sph * SPH_ORG_W, h.n_light * h.n_sph * SPH_ORG_W * 8);
-    copy4(h.l_occ, S.itab + h.i_occ, h.n_light * h.n_sph * h.n_chunk * 2); // 8-byte aligned in the int table
+    copy4(h.l_occ, S.itab + h.i_occ, h.n_light * h.n_sph * h.n_chunk * 2); // 1 cell; 8-byte aligned in the int table
     copy4(h.l_id, S.itab + h.i_sph_id, h.n_sph);
     copy16(h.l_sphb, S.tab + h.o_sph_b, h.n_sph * SPH_B_W * 8);
     __syncthreads();
@@ -1052,6 +1053,21 @@ __device__ __forceinline__ Target make_target(const Scene &S, int obj, bool acti
     return T;
 }
 
+// Direction cell of a shadow ray sd from a light towards a target sphere (q = light - centre,
+// the target's per-origin row): the signs of (sd - a) along the two world axes on which
+// a = -q/|q|, the cone's axis, is shortest (binary32; the host's masks are built for the same
+// cells, each widened by OCC_CELL_EPS, far above this evaluation's error, so a ray near a cell
+// border is covered by the mask of either side).  Mirrored bit for bit by occ_cell_host.
+__device__ __forceinline__ int occ_cell(const double *q, const D3 &sd) {
+    const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
+    const float D = __builtin_sqrtf(qx * qx + qy * qy + qz * qz);
+    const float ax = __builtin_fabsf(qx), ay = __builtin_fabsf(qy), az = __builtin_fabsf(qz);
+    const int drop = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+    const float ex = (float)sd.x * D + qx, ey = (float)sd.y * D + qy, ez = (float)sd.z * D + qz;
+    const float ei = drop == 0 ? ey : ex, ej = drop == 2 ? ey : ez;
+    return (ei >= 0.0f ? 1 : 0) + (ej >= 0.0f ? 2 : 0);
+}
+
 // SPH: the scene holds only spheres and culling is on (host-checked), so every target is a
 // sphere with occluder masks: the cone and triangle/plane paths are compiled out (registers).
 template <int SPH = 0>
@@ -1064,11 +1080,13 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
     // t* of the target itself along the shadow ray
     double ts = 0;
     bool valid = false;
+    int cell = 0;
     if (active) {
         if (SPH || kind == K_SPHERE) {
             const double *q = org_row<SPH>(S, org, loc);
             double B = 2 * (sd.x * q[0] + sd.y * q[1] + sd.z * q[2]);
             valid = sph_t(B, q[3], A4, ts);
+            if (SPH != 2 && h.occ_cells > 1) cell = occ_cell(q, sd); // (staged scenes: one cell)
         } else if (kind == K_TRIANGLE) {
             const double *g = S.tab + h.o_tri + loc * TRI_W;
             const double *q = S.tab + h.o_tri_org + (org * h.n_tri + loc) * TRI_ORG_W;
@@ -1098,7 +1116,8 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
             // per-lane candidate count, not the size of the union over the wave's targets
             // (which grows with every distinct target an incoherent wave holds).
             const unsigned long long *occ = occ_masks<SPH>(S, light, chunk >> 6);
-            unsigned long long mine = blocked ? 0ull : occ[loc * h.n_chunk]; // never holds the target
+            const int ncell = SPH == 2 ? 1 : h.occ_cells;
+            unsigned long long mine = blocked ? 0ull : occ[(loc * ncell + cell) * h.n_chunk]; // never holds the target
             for (;;) {
                 const bool w = !blocked && mine != 0;
                 if (__ballot(w) == 0) break;

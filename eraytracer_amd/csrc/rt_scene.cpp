@@ -89,6 +89,17 @@ int fill_canon(rt_elem *e, uint32_t n) {
 }
 
 // resolve canon chains to the first element of each equality class
+// Bytes of the LDS-staged tables of a spheres-only scene (the layout below, in rt_compile).
+static long stage_bytes(const SceneHdr &h, int ncell) {
+    auto up16 = [](long v) { return (v + 15) / 16 * 16; };
+    long off = up16((long)h.n_obj * OBJ_W * 8);
+    off = up16(off + (long)h.n_obj * OBJ_META_W * 4);
+    off = up16(off + (long)h.n_light * h.n_sph * SPH_ORG_W * 8);
+    off = up16(off + (long)h.n_light * h.n_sph * ncell * h.n_chunk * 8);
+    off = up16(off + (long)h.n_sph * 4);
+    return up16(off + (long)h.n_sph * SPH_B_W * 8);
+}
+
 static int root(const std::vector<rt_elem> &e, int i) {
     while (e[i].canon >= 0 && e[i].canon != i) i = e[i].canon;
     return i;
@@ -542,13 +553,25 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
         }
         it.insert(it.end(), {kind, local, compact[r], rlocal});
     }
-    // Occluder masks, per (light, target sphere).  Shadow rays to a target sphere t start at the
-    // light L and point into the cone from L around ball(c_t, r_t); the target's own t* (its
-    // entry point) is at most |c_t - L|.  Sphere j can block such a ray only if (a) it meets that
-    // cone (angular test as in the kernel's beam culling, with CULL_EPS margins in the safe
-    // direction) and (b) some point of it is within |c_t - L| of L.  The target itself never
-    // blocks (its t equals t* and its list position is not earlier).
+    // Occluder masks, per (light, target sphere, direction cell).  Shadow rays to a target
+    // sphere t start at the light L and point into the cone from L around ball(c_t, r_t); the
+    // target's own t* (its entry point) is at most |c_t - L|.  Sphere j can block such a ray only
+    // if (a) it meets that cone (angular test as in the kernel's beam culling, with CULL_EPS
+    // margins in the safe direction) and (b) some point of it is within |c_t - L| of L.  The
+    // target itself never blocks (its t equals t* and its list position is not earlier).
+    // Cells (the kernel's occ_cell): the cone is split by the signs of dir - a along two world
+    // axes i, j (a = (c_t - L)/|c_t - L|; the axes on which a is shortest, chosen from the
+    // binary32 components of L - c_t exactly as the kernel chooses them).  Sphere j stays in cell
+    // (b_i, b_j) only if its cone of directions (axis w, sin of its half-angle sr) reaches the
+    // half-spaces s*(dir_k - a_k) >= -OCC_CELL_EPS, s = +1 for b_k = 1 and -1 for b_k = 0: the
+    // largest s*dir_k over the cone is cos(max(0, angle(w, s*e_k) - rho)).
     h.n_chunk = (h.n_sph + 63) / 64;
+    // Small scenes and scenes whose tables are staged in LDS (below) keep one cell: their walks
+    // are short (S64: 1.37 steps per test) and the cells' extra LDS and binary32 work cost more
+    // than they save (measured: config 3 -5 %); large scenes get OCC_CELLS (config 5: +4 %).
+    const bool stage_kind = h.cull_ok && h.n_tri == 0 && h.n_pl == 0 && h.n_sph > 0 && h.n_light > 0;
+    h.occ_cells = (h.n_sph < OCC_CELLS_MIN_SPHERES || (stage_kind && stage_bytes(h, 1) <= LDS_STAGE_MAX)) ? 1 : OCC_CELLS;
+    const int ncell = h.occ_cells;
     while (it.size() % 2) it.push_back(0);
     h.i_occ = (int)it.size();
     if (h.cull_ok && h.n_sph > 0) {
@@ -563,18 +586,26 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
                 const double st = wide ? 1.0 : rt / D * (1 + CULL_EPS) + CULL_EPS;
                 const double ct = st >= 1.0 ? 0.0 : std::sqrt(1 - st * st) - CULL_EPS;
                 const double tmax = D * (1 + CULL_EPS) + CULL_EPS;
-                std::vector<uint64_t> m(h.n_chunk, 0);
+                // the kernel's cell axes, from the binary32 components of its row (L - c_t)
+                const float qx = (float)(L.x - T.center.x), qy = (float)(L.y - T.center.y),
+                            qz = (float)(L.z - T.center.z);
+                const float fx = std::fabs(qx), fy = std::fabs(qy), fz = std::fabs(qz);
+                const int drop = (fx >= fy && fx >= fz) ? 0 : (fy >= fz ? 1 : 2);
+                const int axi = drop == 0 ? 1 : 0, axj = drop == 2 ? 1 : 2;
+                const double a3[3] = {ax / D, ay / D, az / D};
+                std::vector<uint64_t> m((size_t)ncell * h.n_chunk, 0);
                 for (size_t j = 0; j < sph.size(); j++) {
                     if ((int)sph[j] == ti) continue;
                     const auto &S = e[sph[j]].u.sphere;
                     const double vx = S.center.x - L.x, vy = S.center.y - L.y, vz = S.center.z - L.z;
                     const double vl = std::sqrt(vx * vx + vy * vy + vz * vz);
                     const double r = std::fabs(S.radius);
-                    bool keep;
+                    bool keep, cells = false;
+                    double sr = 1.0;
                     if (wide || st >= 1.0 || !(ct > 0.0) || vl <= r * (1 + CULL_EPS) + CULL_EPS) {
                         keep = true;
                     } else {
-                        const double sr = r / vl * (1 + CULL_EPS) + CULL_EPS;
+                        sr = r / vl * (1 + CULL_EPS) + CULL_EPS;
                         if (sr >= 1.0) {
                             keep = true;
                         } else {
@@ -582,10 +613,23 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
                             const double thr = ct * cr - st * sr;
                             const double av = (ax * vx + ay * vy + az * vz) / D;
                             keep = !(av + CULL_EPS * vl < thr * vl);
+                            cells = true;
                         }
                     }
                     const double dlow = (vl - r) - CULL_EPS * (vl + r) - CULL_EPS;
-                    if (keep && !(dlow > tmax)) m[j / 64] |= 1ull << (j % 64);
+                    if (!keep || dlow > tmax) continue;
+                    const double w3[3] = {vx / vl, vy / vl, vz / vl};
+                    const double rho = std::asin(sr) + CULL_EPS;
+                    auto reach = [&](int k, double s) { // the cone reaches s*(dir_k - a_k) >= -eps
+                        const double psi = std::acos(std::max(-1.0, std::min(1.0, s * w3[k])));
+                        const double top = psi <= rho ? 1.0 : std::cos(psi - rho);
+                        return !(top + 1e-7 < s * a3[k] - (double)OCC_CELL_EPS);
+                    };
+                    for (int c = 0; c < ncell; c++) {
+                        const double si = (c & 1) ? 1.0 : -1.0, sj = (c & 2) ? 1.0 : -1.0;
+                        if (!cells || ncell == 1 || (reach(axi, si) && reach(axj, sj)))
+                            m[(size_t)c * h.n_chunk + j / 64] |= 1ull << (j % 64);
+                    }
                 }
                 for (uint64_t w : m) {
                     it.push_back((int)(uint32_t)(w & 0xffffffffu));
@@ -615,7 +659,7 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
     // LDS staging layout (16-byte aligned sections)
     h.l_obj = h.l_meta = h.l_org = h.l_occ = h.l_id = h.l_sphb = -1;
     h.l_bytes = 0;
-    if (h.cull_ok && h.n_tri == 0 && h.n_pl == 0 && h.n_sph > 0 && h.n_light > 0) {
+    if (stage_kind && h.occ_cells == 1) {
         auto up16 = [](long v) { return (v + 15) / 16 * 16; };
         long off = 0;
         const long l_obj = off; off = up16(off + (long)h.n_obj * OBJ_W * 8);
