@@ -49,7 +49,7 @@ constexpr int OBJ_META_W = 4; // kind, local index within its type, canon compac
 // Shadow rays from a light into the cone around a target sphere are split into OCC_CELLS
 // direction cells (occ_cell); each cell has its own, smaller, occluder mask.
 #ifndef RT_OCC_CELLS
-#define RT_OCC_CELLS 4 // 1: one mask per (light, target), as before the cells
+#define RT_OCC_CELLS 16 // 4: signs only; 1: one mask per (light, target), as before the cells
 #endif
 constexpr int OCC_CELLS = RT_OCC_CELLS;
 constexpr float OCC_CELL_EPS = 1.0e-4f; // cells overlap by this much (unit-vector components)

@@ -1054,10 +1054,12 @@ __device__ __forceinline__ Target make_target(const Scene &S, int obj, bool acti
 }
 
 // Direction cell of a shadow ray sd from a light towards a target sphere (q = light - centre,
-// the target's per-origin row): the signs of (sd - a) along the two world axes on which
-// a = -q/|q|, the cone's axis, is shortest (binary32; the host's masks are built for the same
-// cells, each widened by OCC_CELL_EPS, far above this evaluation's error, so a ray near a cell
-// border is covered by the mask of either side).  Mirrored bit for bit by occ_cell_host.
+// C: the target's per-origin row): along the two world axes i, j on which a = -q/|q|, the
+// cone's axis, is shortest, the signs of (sd - a) and (16 cells) whether |sd - a| exceeds half
+// the cone's sine r/(2|q|) (r^2 = |q|^2 - C).  Evaluated in binary32; the host's masks are built
+// for the same cells, each widened by OCC_CELL_EPS, far above this evaluation's error, so a ray
+// near a cell border is covered by the mask of either side.  Only the axis choice must agree
+// exactly, and it is the same binary32 comparison on both sides (rt_scene.cpp).
 __device__ __forceinline__ int occ_cell(const double *q, const D3 &sd) {
     const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
     const float D = __builtin_sqrtf(qx * qx + qy * qy + qz * qz);
@@ -1065,7 +1067,12 @@ __device__ __forceinline__ int occ_cell(const double *q, const D3 &sd) {
     const int drop = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
     const float ex = (float)sd.x * D + qx, ey = (float)sd.y * D + qy, ez = (float)sd.z * D + qz;
     const float ei = drop == 0 ? ey : ex, ej = drop == 2 ? ey : ez;
-    return (ei >= 0.0f ? 1 : 0) + (ej >= 0.0f ? 2 : 0);
+    int cell = (ei >= 0.0f ? 1 : 0) + (ej >= 0.0f ? 2 : 0);
+    if (OCC_CELLS == 16) {
+        const float t2 = (float)(((q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) - q[3]) * 0.25); // (r/2)^2
+        cell += (ei * ei >= t2 ? 4 : 0) + (ej * ej >= t2 ? 8 : 0);
+    }
+    return cell;
 }
 
 // SPH: the scene holds only spheres and culling is on (host-checked), so every target is a

@@ -620,14 +620,23 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
                     if (!keep || dlow > tmax) continue;
                     const double w3[3] = {vx / vl, vy / vl, vz / vl};
                     const double rho = std::asin(sr) + CULL_EPS;
-                    auto reach = [&](int k, double s) { // the cone reaches s*(dir_k - a_k) >= -eps
+                    // the cone of sphere j reaches s*(dir_k - a_k) in [lo, hi] (widened by eps):
+                    // its largest s*dir_k is cos(max(0, psi - rho)), its smallest cos(min(pi, psi + rho))
+                    const double eps = OCC_CELL_EPS, tau = rt / D * 0.5; // the kernel's |sd - a| split
+                    auto reach = [&](int k, double s, bool outer, bool split) {
                         const double psi = std::acos(std::max(-1.0, std::min(1.0, s * w3[k])));
                         const double top = psi <= rho ? 1.0 : std::cos(psi - rho);
-                        return !(top + 1e-7 < s * a3[k] - (double)OCC_CELL_EPS);
+                        const double bot = psi + rho >= M_PI ? -1.0 : std::cos(psi + rho);
+                        const double lo = split && outer ? tau - eps : -eps;
+                        if (top + 1e-7 < s * a3[k] + lo) return false;
+                        if (split && !outer && bot - 1e-7 > s * a3[k] + tau + eps) return false;
+                        return true;
                     };
                     for (int c = 0; c < ncell; c++) {
                         const double si = (c & 1) ? 1.0 : -1.0, sj = (c & 2) ? 1.0 : -1.0;
-                        if (!cells || ncell == 1 || (reach(axi, si) && reach(axj, sj)))
+                        const bool split = ncell == 16;
+                        if (!cells || ncell == 1 ||
+                            (reach(axi, si, (c & 4) != 0, split) && reach(axj, sj, (c & 8) != 0, split)))
                             m[(size_t)c * h.n_chunk + j / 64] |= 1ull << (j % 64);
                     }
                 }
