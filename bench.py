@@ -9,7 +9,12 @@ gathered to rank 0 over RCCL, then put back in row order.  Inputs (the compiled 
 are resident in HBM before the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scene s64] [--size 4096] [--depth 5]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+With --gpus N > 1 outside torch.distributed.run (no WORLD_SIZE in the environment), bench.py
+starts ``python -m torch.distributed.run --nnodes 1 --nproc-per-node N --master-addr 127.0.0.1
+--master-port <free> bench.py <same arguments>`` as a child process, before anything touches
+the GPU, and exits with its return code (it does not exec).
 
 Rank 0 prints ONE JSON line.  Extra keys: "roofline" (the binding FP64-VALU roofline of
 the render kernel), "roofline_hbm" (the memory roofline the north star asks for),
@@ -23,6 +28,8 @@ import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -66,6 +73,27 @@ def parse():
     ap.add_argument("--gather", default="compact", choices=["compact", "dense"],
                     help="N > 1: compact = background pixels not sent (rt_slab_pack, default); dense = whole slabs")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(argv, nproc: int, port: int):
+    """The torch.distributed.run command that runs this script with one rank per GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def self_launch(argv, nproc: int, run=subprocess.run) -> int:
+    """Run the N-rank bench as a child process (the caller has not touched the GPU) and
+    return its exit code."""
+    r = run(launcher_cmd(argv, nproc, free_port()))
+    return int(r.returncode)
 
 
 def cpu_baseline(scene, W, H, depth, target_s, spp=1, seed=0):
@@ -164,6 +192,9 @@ def f64_insts(c):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # python3 bench.py --gpus N: start the N ranks ourselves (nothing has touched HIP yet)
+        sys.exit(self_launch(sys.argv[1:], args.gpus))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -176,8 +207,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("bench.py: --gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (one rank per GPU)")
     torch.cuda.set_device(local)
     if world > 1:
         # RCCL brings its own stream(s); with torch's and the library's two shading side streams

@@ -28,6 +28,7 @@ RT_MAX_DEPTH = 16
 RT_MAX_SHARDS = 64
 RT_CFG_SIDE_STREAMS = 1
 RT_CFG_KERNEL_TIMING = 2
+RT_CFG_CULL = 3
 RT_KT_PRIMARY, RT_KT_LEVEL1, RT_KT_RENDER = 1, 2, 4
 
 # every symbol include/rt_mi355x.h declares (tests/test_boundary.py checks the export list)

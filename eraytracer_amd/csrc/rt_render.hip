@@ -1398,7 +1398,9 @@ __global__ __launch_bounds__(256) void k_selftest_math(unsigned long long n, uns
 // =====================================================================================
 struct rt_prepared {
     int device;
-    SceneHdr hdr;
+    SceneHdr hdr;      // what the kernels get: hdr_full, with the filters off when cull == 0
+    SceneHdr hdr_full; // the compiled scene's header
+    int cull = 1;      // rt_configure(RT_CFG_CULL)
     double *d_tab;
     int *d_itab;
     // wavefront-engine work space, grown on demand (one rt_launch in flight per rt_prepared)
@@ -1466,6 +1468,19 @@ struct DevGuard { // restore the caller's current device on scope exit
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 };
+
+// RT_CFG_CULL = 0: every scan tests every object (no wave beams or cones, no occluder masks, no
+// BVH, no LDS-staged tables) — the reference's brute-force scans, against which the filters'
+// frames are checked bit for bit (tests/test_gpu_frames.py).
+void apply_cull(rt_prepared *p) {
+    p->hdr = p->hdr_full;
+    if (!p->cull) {
+        p->hdr.cull_ok = 0;
+        p->hdr.beam_ok = 0;
+        p->hdr.bvh_ok = 0;
+        p->hdr.l_bytes = 0;
+    }
+}
 
 constexpr size_t KT_RING = 64;
 int kt_index(int kernel) { return kernel == RT_KT_PRIMARY ? 0 : kernel == RT_KT_LEVEL1 ? 1 : kernel == RT_KT_RENDER ? 2 : -1; }
@@ -1605,7 +1620,8 @@ int rt_prepare(const rt_elem *scene, uint32_t n, int device, rt_prepared **out) 
     rt_prepared *p = new (std::nothrow) rt_prepared();
     if (!p) return RT_ENOMEM;
     p->device = device;
-    p->hdr = c.hdr;
+    p->hdr_full = c.hdr;
+    apply_cull(p);
     if (hipMalloc(&p->d_tab, c.tab.size() * sizeof(double)) != hipSuccess) {
         delete p;
         return RT_ENOMEM;
@@ -1651,7 +1667,8 @@ int rt_prepare_scene(rt_prepared *p, const rt_elem *scene, uint32_t n) {
     (void)hipFree(p->d_itab);
     p->d_tab = tab;
     p->d_itab = itab;
-    p->hdr = c.hdr;
+    p->hdr_full = c.hdr;
+    apply_cull(p);
     ++p->gen; // captured graphs hold the old tables
     p->last_valid = false;
     return RT_OK;
@@ -1669,6 +1686,13 @@ int rt_configure(rt_prepared *p, int option, int64_t value) {
     case RT_CFG_KERNEL_TIMING:
         if (value < 0 || value > 7) return RT_EBADARG;
         p->timing_mask = (int)value;
+        return RT_OK;
+    case RT_CFG_CULL:
+        if (value < 0 || value > 1) return RT_EBADARG;
+        p->cull = (int)value;
+        apply_cull(p);
+        ++p->gen; // captured graphs hold the old header
+        p->last_valid = false;
         return RT_OK;
     default:
         return RT_EBADARG;

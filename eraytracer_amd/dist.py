@@ -152,19 +152,23 @@ class CompactGather:
     the fixed-size headers are gathered to rank 0 (one collective), which also tells rank 0
     every shard's value count; then each rank sends exactly its non-background values to
     rank 0 (grouped point-to-point, RCCL over xGMI), and rank 0 decodes all shards into the
-    frame.  The exchange runs on a side stream, one frame behind the render: ``submit(i)``
-    issues frame i's header gather, frame i-1's value transfer (after reading its counts on
-    the host — by then frame i is already queued on the GPU) and frame i-2's decode, which it
-    returns on rank 0 (complete once ``frame_ready`` has fired: the decode runs on the side
-    stream, beside the next render).  ``drain()`` finishes the frames in flight.
+    frame.  The exchange runs on a side stream, behind the render: ``submit(i)`` issues frame
+    i's header gather and the copy of its counts to pinned host memory (an event marks the
+    copy), frame i-2's value transfer (its counts read on the host after waiting for that copy
+    event alone — two frames later it has normally long fired, so the host does not stall, and
+    no other work on the side stream is waited for) and frame i-3's decode, which it returns on
+    rank 0 (complete once ``frame_ready`` has fired: the decode runs on the side stream, beside
+    the next render).  ``drain()`` finishes the frames in flight.  The order of collectives is
+    the same on every rank (it depends only on the frame count, never on timing).
 
-    Buffers form a ring of three frames.  Frame i's pack waits for the event that ends frame
-    i-3's send (rank 0: its decode), so the caller may render consecutive frames on different
+    Buffers form a ring of four frames.  Frame i's pack waits for the event that ends frame
+    i-4's send (rank 0: its decode), so the caller may render consecutive frames on different
     streams; every collective is issued on the side stream behind an event of the pack it
     reads, so it never waits for a later render.
     """
 
-    RING = 3
+    RING = 4
+    LAG = 2  # frames between a frame's header gather and its value transfer
 
     def __init__(self, codec, world, rank, slab_elems, dtype, device, frame, group=None):
         import torch
@@ -181,11 +185,11 @@ class CompactGather:
             self.ghdr = [mk(world, hb, dt=torch.uint8) for _ in range(self.RING)]
             self.gvals = [mk(world, slab_elems, dt=dtype) for _ in range(self.RING)]
         self.xs = torch.cuda.Stream(device) if self.cuda else None
-        self.counts = torch.zeros(world, dtype=torch.int64, pin_memory=self.cuda)
+        self.counts = [torch.zeros(world, dtype=torch.int64, pin_memory=self.cuda) for _ in range(self.RING)]
         self.i = 0
         self.free = [None] * self.RING      # event: the slot's last send (decode on rank 0) is done
         self.frame_ready = None             # rank 0: the last returned frame is complete after this
-        self.headed = []   # (ring slot, header gather work)
+        self.headed = []   # (ring slot, event of its counts' copy to the host)
         self.moving = []   # (ring slot, value transfer works)
 
     def _side(self):
@@ -205,7 +209,7 @@ class CompactGather:
             ev = torch.cuda.Event()
             ev.record()
         out = None
-        if self.headed:
+        if len(self.headed) >= self.LAG:
             self._send(*self.headed.pop(0))
         if len(self.moving) > 1:
             out = self._finish(*self.moving.pop(0))
@@ -225,26 +229,33 @@ class CompactGather:
         return out
 
     def _gather_headers(self, b, ev):
+        """Frame slot b: gather the headers to rank 0, then copy the value counts (the first
+        8 bytes of each header) to pinned host memory; the copy's event is kept for _send."""
+        torch = self.torch
         import torch.distributed as dist
         with self._side():
             if ev is not None:
                 self.xs.wait_event(ev)
             gl = list(self.ghdr[b].unbind(0)) if self.rank == 0 else None
             w = dist.gather(self.hdr[b], gather_list=gl, dst=0, group=self.group, async_op=True)
-        self.headed.append((b, w))
-
-    def _send(self, b, work):
-        """Frame in slot b: its counts to the host, then the values to rank 0."""
-        torch = self.torch
-        import torch.distributed as dist
-        with self._side():
-            work.wait()
+            w.wait()  # RCCL: the side stream waits for the gather (gloo: the host does)
             src = self.ghdr[b][:, :8] if self.rank == 0 else self.hdr[b][:8].unsqueeze(0)
             cnt = src.contiguous().view(torch.int64).flatten()
-            self.counts[: cnt.numel()].copy_(cnt, non_blocking=self.cuda)
+            self.counts[b][: cnt.numel()].copy_(cnt, non_blocking=self.cuda)
+            cev = None
             if self.cuda:
-                self.xs.synchronize()
-            counts = [int(c) for c in self.counts.tolist()]
+                cev = torch.cuda.Event()
+                cev.record()
+        self.headed.append((b, cev))
+
+    def _send(self, b, cev):
+        """Frame in slot b: read its counts on the host (waiting for their copy alone), then
+        send the values to rank 0."""
+        import torch.distributed as dist
+        with self._side():
+            if cev is not None:
+                cev.synchronize()
+            counts = [int(c) for c in self.counts[b].tolist()]
             # at least one pixel per message: every rank takes part in every batch
             n = [max(c, 1) * 3 for c in counts]
             ops = []
@@ -324,11 +335,12 @@ class FrameRenderer:
     walk); the next frames' dense primary and shading kernels fill it.  Each context then
     runs its kernels on its slot's stream alone (RT_CFG_SIDE_STREAMS = 0), so the process
     stays within its hardware queues.  ``stream`` is the stream of the last launched frame;
-    work on that frame (the gather's pack) goes on it."""
+    work on that frame (the gather's pack) goes on it.  ``cull=False`` renders with brute-force
+    scans (RT_CFG_CULL = 0: every object tested by every ray; same bits, many times slower)."""
 
     def __init__(self, scene, width: int, height: int, depth: int, *, rank: int = 0, world: int = 1,
                  device: int = 0, row_block: int = 16, precision: str = "f32", order: str = "exact", group=None,
-                 levels: bool = False, spp: int = 1, seed: int = 0, inflight: int = 1):
+                 levels: bool = False, spp: int = 1, seed: int = 0, inflight: int = 1, cull: bool = True):
         import torch
         self.torch = torch
         self.L = N.lib()
@@ -350,6 +362,8 @@ class FrameRenderer:
             self._ps.append(p)
             if inflight > 1:
                 N.check(self.L.rt_configure(p, N.RT_CFG_SIDE_STREAMS, 0), "rt_configure")
+            if not cull:  # brute-force scans (RT_CFG_CULL = 0): the filters' bit-for-bit check
+                N.check(self.L.rt_configure(p, N.RT_CFG_CULL, 0), "rt_configure")
         self._p = self._ps[0]
         self.slabs = [torch.empty((self.rows, width, 3), dtype=self.dtype, device=self.device)
                       for _ in range(inflight)]

@@ -225,6 +225,12 @@ int rt_release(rt_prepared *p);
 #define RT_KT_LEVEL1 2   /* the level-0 shading + level-1 reflection pass (k_reflect_shade(1); with
                             side streams or levels: k_reflect(1)) */
 #define RT_KT_RENDER 4   /* k_render: the fused engine's one kernel per frame */
+/* RT_CFG_CULL: 1 = the default: scans skip objects a conservative filter proves cannot be hit
+ *   (wave beams and shadow cones, per-light occluder masks, the sphere BVH); 0 = brute force,
+ *   every nearest scan and every shadow test visits every object of the scene, as the
+ *   reference's scans do (raytracer.erl:303-346, :256-267).  Both give the same bits; 0 exists
+ *   to check that (it is many times slower). */
+#define RT_CFG_CULL 3
 int rt_configure(rt_prepared *p, int option, int64_t value);
 int rt_kernel_time(rt_prepared *p, int kernel, double *total_ms, uint64_t *launches, int reset);
 /* ---- compact slab transfer (the multi-GPU gather; raytracer.erl:151-161 collects pixels) --

@@ -115,17 +115,19 @@ def test_config5_s256_4096_d8_spp16_rows(oracle):
         _compare(img[r:r + 1], lv[r:r + 1], ref, rlv, f"config 5 row {r}", max(4, W * BOUND_FRAC))
 
 
-@pytest.mark.parametrize("name,w,h,d", [("default_powers", 320, 240, 5), ("default_powers", 97, 61, 1),
-                                        ("mixed", 256, 192, 5)])
-def test_general_pow_and_mixed_scenes(oracle, name, w, h, d):
+# (scene, w, h, depth, bound on the pixels not bit-identical): measured round 3 on MI355X
+# (default_powers 320x240 d5: 1631, 97x61 d1: 185, mixed 256x192 d5: 1374), bound = x1.5
+@pytest.mark.parametrize("name,w,h,d,bound", [("default_powers", 320, 240, 5, 2450), ("default_powers", 97, 61, 1, 280),
+                                              ("mixed", 256, 192, 5, 2060)])
+def test_general_pow_and_mixed_scenes(oracle, name, w, h, d, bound):
     """Specular powers 0, 0.5, 2.5, 1025 (the general math:pow/2 path, :289, and pow(0,0)=1.0)
     on the fused engine (default scene) and a mixed 58-object scene on the wavefront engine.
-    Device pow vs host libm may differ by an ulp (measured 2-3 % of pixels differ, by <= 1e-14):
-    the bound allows 5 %, the bar does not move."""
+    Device pow (~1 ulp) vs host libm differ by an ulp on 2-3 % of the pixels (<= 1e-14): the
+    bound is the measured count plus half, the 1e-5 bar does not move."""
     scene = scenes.named(name)
     img, lv = render(w, h, scene, d, levels=True)
     ref, rlv = oracle.render(N.marshal(scene), w, h, d, mode=oracle.MEMO, levels=True)
-    _compare(img, lv, ref, rlv, name, w * h // 20)
+    _compare(img, lv, ref, rlv, name, bound)
 
 
 def test_fused_wavefront_kernels_all_paths():
