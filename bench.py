@@ -174,15 +174,11 @@ DOMINANT = {"wave": ("k_reflect_shade#0", "RT_KT_LEVEL1",
             "fused": ("k_render#0", "RT_KT_RENDER", "k_render: the fused engine's one kernel per frame")}
 
 
-def engine_of(counts, spp):
-    """The engine rt_launch picks (rt_render.hip use_mega_engine; RT_ENGINE forces one)."""
-    env = os.environ.get("RT_ENGINE")
-    if env in ("fused", "mega"):
-        return "fused"
-    if env == "wave" or spp > 1:
-        return "wave"
-    n_obj = counts["spheres"] + counts["triangles"] + counts["planes"]
-    return "fused" if n_obj <= int(os.environ.get("RT_FUSED_MAX_OBJECTS", "40")) else "wave"
+def engine_of(N, fr, spp):
+    """The engine rt_launch runs for this context (rt_engine: the library's own decision,
+    RT_ENGINE / RT_FUSED_MAX_OBJECTS included)."""
+    e = N.check(N.lib().rt_engine(fr._ps[0], spp), "rt_engine")
+    return "fused" if e == N.RT_ENGINE_FUSED else "wave"
 
 
 def f64_insts(c):
@@ -281,7 +277,7 @@ def main():
     # GPU time of the timed region: HIP events on the caller's stream, every in-flight slot
     # stream forked from it after the start event and joined into it before the end event;
     # the dominant kernel's launches are bracketed by events on their own streams
-    engine = engine_of(counts, args.spp)
+    engine = engine_of(N, fr, args.spp)
     dom_label, dom_kt, dom_desc = DOMINANT[engine]
     fr.time_kernels(getattr(N, dom_kt))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -490,8 +486,10 @@ def self_check(fr, pipe, scene, args, rank, world, local):
 def boundary_legs(N, scene, W, H, args):
     """The C-ABI boundary the BEAM NIF uses (rt_render: persistent context, row bands whose
     copies overlap the next band's render), timed warm (C-side total_ms, best of 3): into pinned
-    memory (rt_host_alloc — what the NIF hands the BEAM as a resource binary) and into fresh
-    pageable memory; plus raytrace/5 natively (render + P3 text on the GPU + file)."""
+    memory (rt_host_alloc — what the NIF hands the BEAM as a resource binary) without levels
+    (render_binary) and with the primary-hit mask (RT_LEVELS_HIT: render_frame, what the
+    strategy funs call), into fresh pageable memory; plus raytrace/5 natively (render + P3 text on
+    the GPU + file)."""
     import numpy as np
 
     from eraytracer_amd.raytracer import render, render_ppm_file
@@ -499,12 +497,13 @@ def boundary_legs(N, scene, W, H, args):
     dt = np.float32 if args.precision == "f32" else np.float64
     frame_px = W * H
     pinned = N.pinned_empty((H, W, 3), dt)
-    for name, dst in (("boundary_mpx_s", pinned), ("boundary_pageable_mpx_s", None)):
+    for name, dst, lv in (("boundary_mpx_s", pinned, False), ("boundary_hit_mask_mpx_s", pinned, "hit"),
+                          ("boundary_pageable_mpx_s", None, False)):
         ts = []
         for i in range(4):
             st = {}
             render(W, H, scene, args.depth, precision=args.precision, order=args.order, stats=st, spp=args.spp,
-                   seed=args.seed, out=dst)
+                   seed=args.seed, out=dst, levels=lv)
             if i:
                 ts.append(st["total_ms"])
         out[name] = round(frame_px / (min(ts) / 1e3) / 1e6, 3)

@@ -30,6 +30,8 @@ RT_CFG_SIDE_STREAMS = 1
 RT_CFG_KERNEL_TIMING = 2
 RT_CFG_CULL = 3
 RT_KT_PRIMARY, RT_KT_LEVEL1, RT_KT_RENDER = 1, 2, 4
+RT_LEVELS_HIT = 1
+RT_ENGINE_WAVE, RT_ENGINE_FUSED = 0, 1
 
 # every symbol include/rt_mi355x.h declares (tests/test_boundary.py checks the export list)
 EXPORTS = (
@@ -37,7 +39,7 @@ EXPORTS = (
     "rt_render", "rt_prepare", "rt_shard_rows", "rt_launch", "rt_launch_spp", "rt_unshard", "rt_configure", "rt_release",
     "rt_ppm_bound", "rt_ppm_format", "rt_render_ppm_file",
     "rt_slab_header_bytes", "rt_slab_pack", "rt_slab_unpack", "rt_selftest_math",
-    "rt_host_alloc", "rt_host_free", "rt_reset_contexts", "rt_kernel_time",
+    "rt_host_alloc", "rt_host_free", "rt_reset_contexts", "rt_kernel_time", "rt_engine",
 )
 
 
@@ -84,7 +86,7 @@ class RtOpts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("first_dev", ctypes.c_int32), ("ndev", ctypes.c_int32),
                 ("precision", ctypes.c_int32), ("order", ctypes.c_int32), ("row_block", ctypes.c_uint32),
                 ("out_levels", ctypes.c_void_p), ("spp", ctypes.c_uint32), ("nshards", ctypes.c_uint32),
-                ("seed", ctypes.c_uint64)]
+                ("seed", ctypes.c_uint64), ("flags", ctypes.c_uint32)]
 
 
 class RtStats(ctypes.Structure):
@@ -138,6 +140,7 @@ def lib() -> ctypes.CDLL:
     L.rt_unshard.argtypes = [vp, u32, u32, u32, u32, i32, vp, vp]
     L.rt_release.argtypes = [vp]
     L.rt_configure.argtypes = [vp, i32, ctypes.c_int64]
+    L.rt_engine.argtypes = [vp, u32]
     L.rt_selftest_math.argtypes = [i32, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     L.rt_slab_header_bytes.restype = ctypes.c_size_t
     L.rt_slab_header_bytes.argtypes = [u32, u32, u32, u32]

@@ -498,7 +498,7 @@ int rt_render(const rt_elem *scene, uint32_t n, uint32_t width, uint32_t height,
             for (uint32_t b = 0; b < nb && err == RT_OK; ++b) {
                 const uint32_t b0 = b * band, b1 = std::min(slab, b0 + band);
                 err = rt_launch_rows(c->p, width, height, depth, rb, s, ns, o.precision, o.order, o.spp, o.seed, b0,
-                                     b1, slab_out, slab_lv, c->render);
+                                     b1, slab_out, slab_lv, c->render, (o.flags & RT_LEVELS_HIT) ? 1 : 0);
                 if (err == RT_OK && hipEventRecord(c->band[i * nb + b], c->render) != hipSuccess) err = RT_EHIP;
                 if (err == RT_OK && pinned) {
                     hipStream_t cs = ((i * nb + b) % copy_streams()) ? c->copy2 : c->copy;

@@ -10,9 +10,11 @@
 
 // rt_launch_spp restricted to slab rows [row_begin, min(row_end, slab rows)) (rt_render.hip).
 // row_begin must be a multiple of 16 (the tile height); d_out / d_levels point at slab row 0.
+// levels_hit: d_levels gets the primary-hit mask (1 / 0) instead of the level count (RT_LEVELS_HIT).
 int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, uint32_t row_block,
                    uint32_t shard, uint32_t nshards, int precision, int order, uint32_t spp, uint64_t seed,
-                   uint32_t row_begin, uint32_t row_end, void *d_out, uint8_t *d_levels, void *stream);
+                   uint32_t row_begin, uint32_t row_end, void *d_out, uint8_t *d_levels, void *stream,
+                   int levels_hit = 0);
 
 // Replace the scene of a prepared context in place (its work space, streams and events are
 // kept; captured frame graphs are invalidated).  No launch of p may be in flight.

@@ -1241,7 +1241,7 @@ template <int ORDER, int PREC, bool LEVELS, bool GENPOW>
 __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict__ tab,
                                                   const int *__restrict__ itab, int W, int H, int depth, int rb,
                                                   int shard, int nshards, int row0, int row_end, void *__restrict__ out,
-                                                  uint8_t *__restrict__ levels) {
+                                                  uint8_t *__restrict__ levels, int levels_hit) {
     // this launch covers slab rows [row0, row_end); out / levels point at slab row 0
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Scene S{hdr, tab, itab};
@@ -1356,7 +1356,7 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
         float *o = reinterpret_cast<float *>(out) + pix * 3;
         o[0] = (float)col.x; o[1] = (float)col.y; o[2] = (float)col.z;
     }
-    if (LEVELS) levels[pix] = (uint8_t)nlev;
+    if (LEVELS) levels[pix] = (uint8_t)(levels_hit ? (nlev > 0) : nlev);
 }
 
 #include "rt_wave.inc" // the wavefront engine (default)
@@ -1520,16 +1520,16 @@ struct KtScope {
 
 template <int ORDER, int PREC, bool GENPOW>
 int launch_t(rt_prepared *p, int W, int H, int depth, int rb, int shard, int nshards, int row0, int row_end,
-             void *out, uint8_t *levels, hipStream_t st) {
+             void *out, uint8_t *levels, hipStream_t st, int levels_hit) {
     dim3 grid((W + TILE - 1) / TILE, (row_end - row0 + TILE - 1) / TILE);
     size_t lds = ORDER == RT_ORDER_EXACT ? (size_t)depth * BLOCK * 12 : 0;
     KtScope kt(p, RT_KT_RENDER, st);
     if (levels)
         hipLaunchKernelGGL((k_render<ORDER, PREC, true, GENPOW>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
-                           H, depth, rb, shard, nshards, row0, row_end, out, levels);
+                           H, depth, rb, shard, nshards, row0, row_end, out, levels, levels_hit);
     else
         hipLaunchKernelGGL((k_render<ORDER, PREC, false, GENPOW>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
-                           H, depth, rb, shard, nshards, row0, row_end, out, levels);
+                           H, depth, rb, shard, nshards, row0, row_end, out, levels, levels_hit);
     HIPCHK(hipGetLastError());
     return RT_OK;
 }
@@ -1820,8 +1820,12 @@ bool wave_single_write(const rt_prepared *p, int D, bool levels) {
 template <int PREC, bool GENPOW>
 int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns, int row_begin, int row_end, void *out,
                      uint8_t *levels, hipStream_t st, int spp = 1, int sample = 0, unsigned long long seed = 0,
-                     double *acc = nullptr) {
-    // renders slab rows [row_begin, row_end) (row_begin a multiple of TILE); out / levels point at slab row 0
+                     double *acc = nullptr, int levels_hit = 0) {
+    // renders slab rows [row_begin, row_end) (row_begin a multiple of TILE); out / levels point at slab row 0.
+    // levels_hit: k_primary writes the primary-hit mask (what it always writes: 1 on a hit, 0 on a
+    // miss) and the later kernels do not count levels, so the fused path stays on
+    uint8_t *const levels_primary = levels;
+    if (levels_hit) levels = nullptr;
     const int slab_rows = row_end - row_begin;
     const int nlev = D > 0 ? D : 1;
     const size_t per_row = (size_t)W * nlev * sizeof(HitRec);
@@ -1897,6 +1901,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         const size_t off = (size_t)row0 * W;
         void *o = static_cast<char *>(out) + off * 3 * (PREC == RT_OUT_F64 ? 8 : 4);
         uint8_t *lv = levels ? levels + off : nullptr;
+        uint8_t *lv0 = levels_primary ? levels_primary + off : nullptr; // k_primary's
         double *acc_p = acc ? acc + off * 3 : nullptr;
         auto qk = [&](int k) { return q + (size_t)k * ntiles * TILE_SLOTS; };
         auto ck = [&](int k) { return p->d_counts + (size_t)k * ntiles; };
@@ -1911,9 +1916,9 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
         {
             KtScope kt(p, RT_KT_PRIMARY, st);
-            if (lv)
+            if (lv0)
                 hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W,
-                                   H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed, acc_p);
+                                   H, D, rb, sh, ns, rows, row0, o, lv0, q, p->d_counts, ntiles, spp, sample, seed, acc_p);
             else
                 hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
                                    W, H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed, acc_p);
@@ -2137,6 +2142,11 @@ bool use_mega_engine(const rt_prepared *p) {
 
 extern "C" {
 
+int rt_engine(rt_prepared *p, uint32_t spp) {
+    if (!p || spp == 0) return RT_EBADARG;
+    return (spp == 1 && use_mega_engine(p)) ? RT_ENGINE_FUSED : RT_ENGINE_WAVE;
+}
+
 int rt_launch(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, uint32_t row_block, uint32_t shard,
               uint32_t nshards, int precision, int order, void *d_out, uint8_t *d_levels, void *stream) {
     return rt_launch_spp(p, width, height, depth, row_block, shard, nshards, precision, order, 1, 0, d_out, d_levels,
@@ -2147,7 +2157,7 @@ int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dept
                   uint32_t shard, uint32_t nshards, int precision, int order, uint32_t spp, uint64_t seed,
                   void *d_out, uint8_t *d_levels, void *stream) {
     return rt_launch_rows(p, width, height, depth, row_block, shard, nshards, precision, order, spp, seed, 0, ~0u,
-                          d_out, d_levels, stream);
+                          d_out, d_levels, stream, 0);
 }
 
 } // extern "C"
@@ -2157,7 +2167,7 @@ int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dept
 // the next band's render.  row_begin must be a multiple of 16 (the tile height).
 int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t depth, uint32_t row_block,
                    uint32_t shard, uint32_t nshards, int precision, int order, uint32_t spp, uint64_t seed,
-                   uint32_t row_begin, uint32_t row_end, void *d_out, uint8_t *d_levels, void *stream) {
+                   uint32_t row_begin, uint32_t row_end, void *d_out, uint8_t *d_levels, void *stream, int levels_hit) {
     if (!p || !d_out) return RT_EBADARG;
     if (width == 0 && height == 0) return RT_DONE;
     if (width == 0 || height == 0) return RT_EBADARG;
@@ -2195,20 +2205,20 @@ int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dep
         void *dst = static_cast<char *>(d_out) + e0 * (precision == RT_OUT_F64 ? 8 : 4);
         for (int s = 0; s < (int)spp; ++s) {
             uint8_t *lv = s == 0 ? d_levels : nullptr;
-            if (wave_single_write(p, D, lv != nullptr)) {
+            if (wave_single_write(p, D, lv != nullptr && !levels_hit)) {
                 // every pixel written once: the pass folds its sample into acc (and the last one
                 // writes the output) itself — no sample slab, no k_accum
-#define RT_SS(P) (p->hdr.int_pow ? launch_wavefront<P, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, nullptr, st, (int)spp, s, seed, acc) \
-                                 : launch_wavefront<P, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, nullptr, st, (int)spp, s, seed, acc))
+#define RT_SS(P) (p->hdr.int_pow ? launch_wavefront<P, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, lv, st, (int)spp, s, seed, acc, 1) \
+                                 : launch_wavefront<P, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, lv, st, (int)spp, s, seed, acc, 1))
                 rc = precision == RT_OUT_F64 ? RT_SS(RT_OUT_F64) : RT_SS(RT_OUT_F32);
 #undef RT_SS
                 if (rc != RT_OK) return rc;
                 continue;
             }
             rc = p->hdr.int_pow ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, r0, r1, smp, lv, st,
-                                                                      (int)spp, s, seed)
+                                                                      (int)spp, s, seed, nullptr, levels_hit)
                                 : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, r0, r1, smp, lv, st,
-                                                                     (int)spp, s, seed);
+                                                                     (int)spp, s, seed, nullptr, levels_hit);
             if (rc != RT_OK) return rc;
             if (precision == RT_OUT_F64)
                 hipLaunchKernelGGL(k_accum<RT_OUT_F64>, dim3(blocks), dim3(256), 0, st, n, smp + e0, acc + e0, dst, s,
@@ -2222,20 +2232,24 @@ int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dep
     }
     if (!use_mega_engine(p)) { // the wavefront engine always evaluates the reference's exact order
         const long long key[12] = {W, H, D, rb, sh, ns, precision, ((long long)r0 << 32) | r1,
-                                   (long long)(intptr_t)d_out, (long long)(intptr_t)d_levels, 0, 0};
+                                   (long long)(intptr_t)d_out, (long long)(intptr_t)d_levels, levels_hit, 0};
         return launch_frame(p, key, st, [&](hipStream_t s) {
             if (precision == RT_OUT_F64)
                 return p->hdr.int_pow
-                           ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s)
-                           : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s);
+                           ? launch_wavefront<RT_OUT_F64, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s, 1, 0, 0,
+                                                                 nullptr, levels_hit)
+                           : launch_wavefront<RT_OUT_F64, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s, 1, 0, 0,
+                                                                nullptr, levels_hit);
             return p->hdr.int_pow
-                       ? launch_wavefront<RT_OUT_F32, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s)
-                       : launch_wavefront<RT_OUT_F32, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s);
+                       ? launch_wavefront<RT_OUT_F32, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s, 1, 0, 0,
+                                                             nullptr, levels_hit)
+                       : launch_wavefront<RT_OUT_F32, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, s, 1, 0, 0,
+                                                            nullptr, levels_hit);
         });
     }
 #define RT_DISPATCH(O, P)                                                                                          \
-    return p->hdr.int_pow ? launch_t<O, P, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, st)              \
-                          : launch_t<O, P, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, st)
+    return p->hdr.int_pow ? launch_t<O, P, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, st, levels_hit)  \
+                          : launch_t<O, P, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, d_levels, st, levels_hit)
     if (order == RT_ORDER_EXACT) {
         if (precision == RT_OUT_F64) RT_DISPATCH(RT_ORDER_EXACT, RT_OUT_F64);
         RT_DISPATCH(RT_ORDER_EXACT, RT_OUT_F32);

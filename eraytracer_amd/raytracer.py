@@ -62,7 +62,10 @@ def render(width: int, height: int, scene=None, depth: int = 5, *, precision: st
     ``_native.pinned_empty``: pinned memory is written by DMA directly).  ``nshards``: row
     shards of the distributed split (default one per device; shard s on device s % ndev).
     ``spp`` > 1: stochastic supersampling as defined at RT_SUPERSAMPLING in
-    include/rt_mi355x.h (not in the reference; levels then report sample 0)."""
+    include/rt_mi355x.h (not in the reference; levels then report sample 0).
+    ``levels="hit"``: the levels array is the primary-hit mask (1 where the primary ray hits,
+    RT_LEVELS_HIT) instead of the chain's level count — what the strategy funs need for the
+    reference's integer pixels, without turning the fused shading kernels off."""
     if not _sizes_ok(width, height):
         return DONE
     _depth_ok(depth)
@@ -79,7 +82,8 @@ def render(width: int, height: int, scene=None, depth: int = 5, *, precision: st
     lv = np.empty((height, width), dtype=np.uint8) if levels else None
     opts = N.RtOpts(ctypes.sizeof(N.RtOpts), first_dev, ndev, prec,
                     {"exact": N.RT_ORDER_EXACT, "fast": N.RT_ORDER_FAST}[order], row_block,
-                    lv.ctypes.data if levels else None, spp, nshards, seed)
+                    lv.ctypes.data if levels else None, spp, nshards, seed,
+                    N.RT_LEVELS_HIT if levels == "hit" else 0)
     st = N.RtStats()
     rc = L.rt_render(elems, len(elems), width, height, depth, ctypes.byref(opts), out.ctypes.data, ctypes.byref(st))
     if rc == N.RT_DONE:
@@ -99,10 +103,10 @@ def _has_lights(scene) -> bool:
 def _pixel_list(img, lv, scene, keyed: bool):
     """The strategy's result list with the reference's exact term types: the integer zeros
     #colour{r=0,g=0,b=0} where the reference returns them — no primary hit (?BACKGROUND_COLOUR,
-    raytracer.erl:82, :201), depth 0 (:186-187; levels are 0 there) or a scene without point
+    raytracer.erl:82, :201), depth 0 (:186-187; the hit mask is 0 there) or a scene without point
     lights (lighting_function/6 folds from #vector{0,0,0}, :250) — floats everywhere else
     (specular_term's math:pow/2 always yields a float, :289).  Keys: 1 (simple, :95) or
-    X+Y*Width (:112, :173)."""
+    X+Y*Width (:112, :173).  lv: the primary-hit mask or the level counts (0 = no hit either way)."""
     flat = img.reshape(-1, 3).tolist()
     zero = (lv.reshape(-1) == 0) if _has_lights(scene) else np.ones(len(flat), dtype=bool)
     ints = (0, 0, 0)
@@ -116,7 +120,7 @@ def _strategy(Width, Height, Scene, Recursion_depth, keyed, ndev=1):
         return DONE
     if Scene is None:
         Scene = default_scene()
-    img, lv = render(Width, Height, Scene, Recursion_depth, levels=True, ndev=ndev)
+    img, lv = render(Width, Height, Scene, Recursion_depth, levels="hit", ndev=ndev)
     return _pixel_list(img, lv, Scene, keyed)
 
 

@@ -8,15 +8,20 @@
  *
  *   rt_nif:render_frame(Width, Height, Scene, Depth, Opts) -> done | Frame
  *       Opts = #{spp => N, seed => S, devices => all | N}; dirty I/O scheduler.
- *       Frame = {rt_frame, Width, Height, Rgb, Levels, Lights}: Rgb is W*H*3 native-endian
+ *       Frame = {rt_frame, Width, Height, Rgb, Levels, Mode}: Rgb is W*H*3 native-endian
  *       doubles, row-major, in pinned host memory (written by DMA; a resource binary);
- *       Levels is one byte per pixel (reflection-chain levels that hit); Lights is true when
- *       the scene holds a #point_light{}.
+ *       Mode says which pixels are the integer triple {0,0,0} (see below): true = those whose
+ *       primary ray hits nothing (Levels: one byte per pixel, 0 there), false = every pixel
+ *       (no #point_light{} in the scene; Levels is empty), floats = none (spp > 1, a
+ *       supersampled frame, which the reference does not have: every pixel is an average of
+ *       jittered samples, so always three floats; Levels is empty).
  *   rt_nif:pixels_chunk(Frame, Start, Count, KeyMode, Tail) -> [{Key, {R,G,B}} | Tail]
  *       pixels Start .. Start+Count-1 as the reference's list elements, consed onto Tail
  *       (KeyMode = simple: key 1, raytracer.erl:95 | indexed: X+Y*Width, :112, :173).  A normal
- *       scheduler call, bounded work: raytracer_gpu builds the whole list from the end in
- *       chunks, or folds over it chunk by chunk (raytracer_gpu:fold_pixels/4).
+ *       scheduler call of bounded work: Count is at most PIXELS_CHUNK_MAX (4096 pixels, about
+ *       20k terms, well under the 1 ms a normal-scheduler NIF may take), and it reports the
+ *       share of its timeslice it used (enif_consume_timeslice).  raytracer_gpu builds the whole
+ *       list from the end in chunks, or folds over it chunk by chunk (raytracer_gpu:fold_pixels/4).
  *   rt_nif:render_binary(Width, Height, Scene, Depth[, Opts]) -> done | binary()
  *   rt_nif:render_ppm_file(Width, Height, Scene, Depth, Filename) -> ok | done
  *
@@ -24,7 +29,9 @@
  * triple #colour{r=0,g=0,b=0} — no primary hit (?BACKGROUND_COLOUR, raytracer.erl:82, :201),
  * depth 0 (pixel_colour_from_ray/3 clause 1, :186-187), or no point light in the scene
  * (lighting_function/6 folds from #vector{0,0,0}, :250) — is returned as {0,0,0}; every other
- * pixel as three floats (specular_term's math:pow/2 always yields a float, :289).
+ * pixel as three floats (specular_term's math:pow/2 always yields a float, :289).  The
+ * primary-hit mask comes from rt_render's RT_LEVELS_HIT mode (rt_opts.flags), which keeps the
+ * fused wavefront kernels that a full level count would turn off.
  *
  * The scene list is read record by record (raytracer.erl:72-81) accepting an integer or a
  * float in every numeric slot; exact equality (=:=) between list elements, which
@@ -42,7 +49,7 @@
 #include "rt_mi355x.h"
 
 static ERL_NIF_TERM atom_done, atom_simple, atom_indexed, atom_error, atom_rt_frame, atom_true, atom_false,
-    atom_spp, atom_seed, atom_devices, atom_all, atom_ok, atom_enomem;
+    atom_floats, atom_spp, atom_seed, atom_devices, atom_all, atom_ok, atom_enomem;
 static ErlNifResourceType *pinned_type;
 
 /* a block of pinned host memory (rt_host_alloc) owned by the resource binaries made from it */
@@ -68,6 +75,7 @@ static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
     atom_rt_frame = enif_make_atom(env, "rt_frame");
     atom_true = enif_make_atom(env, "true");
     atom_false = enif_make_atom(env, "false");
+    atom_floats = enif_make_atom(env, "floats");
     atom_spp = enif_make_atom(env, "spp");
     atom_seed = enif_make_atom(env, "seed");
     atom_devices = enif_make_atom(env, "devices");
@@ -257,6 +265,9 @@ static int render_common(ErlNifEnv *env, const ERL_NIF_TERM argv[], unsigned spp
         *ret = enif_raise_exception(env, atom_enomem);
         goto out;
     }
+    /* the primary-hit mask, only where it decides a term type: spp = 1 and a lit scene */
+    want_levels = want_levels && spp == 1 && *lights;
+    if (!want_levels) (void)enif_make_new_binary(env, 0, lv); /* an empty Levels binary */
     if (want_levels) {
         if (!enif_alloc_binary((size_t)*W * *H, &lvb)) {
             *ret = enif_raise_exception(env, atom_enomem);
@@ -272,6 +283,7 @@ static int render_common(ErlNifEnv *env, const ERL_NIF_TERM argv[], unsigned spp
     o.order = RT_ORDER_EXACT;
     o.row_block = 16;
     o.out_levels = have_lv ? lvb.data : NULL;
+    o.flags = RT_LEVELS_HIT; /* a hit mask, not level counts: the fused kernels stay on */
     o.spp = spp; /* RT_SUPERSAMPLING (include/rt_mi355x.h); 1 = the reference's pixel */
     o.seed = seed;
     int rc = rt_render(elems, n, *W, *H, D, &o, data, NULL);
@@ -301,11 +313,12 @@ static ERL_NIF_TERM render_frame_nif(ErlNifEnv *env, int argc, const ERL_NIF_TER
     if (!get_opts(env, argv[4], &spp, &seed, &ndev)) return enif_make_badarg(env);
     if (!render_common(env, argv, spp, seed, ndev, 1, &W, &H, &rgb, &lv, &lights, &ret)) return ret;
     ERL_NIF_TERM t[6] = {atom_rt_frame, enif_make_uint(env, W), enif_make_uint(env, H), rgb, lv,
-                         lights ? atom_true : atom_false};
+                         spp > 1 ? atom_floats : lights ? atom_true : atom_false};
     return enif_make_tuple_from_array(env, t, 6);
 }
 
 /* pixels_chunk(Frame, Start, Count, KeyMode, Tail) -> [{Key, {R,G,B}} | Tail] */
+#define PIXELS_CHUNK_MAX 4096
 static ERL_NIF_TERM pixels_chunk_nif(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     const ERL_NIF_TERM *f;
     int arity, keyed;
@@ -317,11 +330,13 @@ static ERL_NIF_TERM pixels_chunk_nif(ErlNifEnv *env, int argc, const ERL_NIF_TER
         !enif_get_uint(env, f[1], &W) || !enif_get_uint(env, f[2], &H) || !enif_inspect_binary(env, f[3], &rgb) ||
         !enif_inspect_binary(env, f[4], &lv))
         return enif_make_badarg(env);
-    const int lights = enif_is_identical(f[5], atom_true);
+    /* mode: true = {0,0,0} where the primary ray misses, false = everywhere, floats = nowhere */
+    const int by_hit = enif_is_identical(f[5], atom_true), floats = enif_is_identical(f[5], atom_floats);
+    if (!by_hit && !floats && !enif_is_identical(f[5], atom_false)) return enif_make_badarg(env);
     const ErlNifUInt64 npx = (ErlNifUInt64)W * H;
-    if (rgb.size != npx * 3 * sizeof(double) || lv.size != npx) return enif_make_badarg(env);
+    if (rgb.size != npx * 3 * sizeof(double) || lv.size != (by_hit ? npx : 0)) return enif_make_badarg(env);
     if (!enif_get_uint64(env, argv[1], &start) || !enif_get_uint64(env, argv[2], &count) || start > npx ||
-        count > npx - start)
+        count > npx - start || count > PIXELS_CHUNK_MAX)
         return enif_make_badarg(env);
     if (enif_is_identical(argv[3], atom_simple)) keyed = 0;
     else if (enif_is_identical(argv[3], atom_indexed)) keyed = 1;
@@ -332,7 +347,7 @@ static ERL_NIF_TERM pixels_chunk_nif(ErlNifEnv *env, int argc, const ERL_NIF_TER
     ERL_NIF_TERM ints = enif_make_tuple3(env, zero, zero, zero);
     for (ErlNifUInt64 i = start + count; i-- > start;) {
         ERL_NIF_TERM c;
-        if (!lights || lv.data[i] == 0) {
+        if (!floats && (!by_hit || lv.data[i] == 0)) {
             c = ints;
         } else {
             const double *p = px + 3 * i;
@@ -341,6 +356,9 @@ static ERL_NIF_TERM pixels_chunk_nif(ErlNifEnv *env, int argc, const ERL_NIF_TER
         }
         list = enif_make_list_cell(env, enif_make_tuple2(env, keyed ? enif_make_uint64(env, i) : one, c), list);
     }
+    /* the share of a 1 ms timeslice this call used (~PIXELS_CHUNK_MAX pixels per slice) */
+    int pct = (int)(count * 100 / PIXELS_CHUNK_MAX);
+    (void)enif_consume_timeslice(env, pct < 1 ? 1 : pct > 100 ? 100 : pct);
     return list;
 }
 

@@ -14,7 +14,8 @@
 %% distributed forms key each pixel by X+Y*Width and sort by key (raytracer.erl:112, :155,
 %% :173), the simple form uses key 1 (raytracer.erl:95); write_pixels_to_ppm/5 ignores keys.
 %% Term types are the reference's too: {0,0,0} integers for background, depth-0 and no-light
-%% pixels, floats elsewhere (rt_nif.c).
+%% pixels, floats elsewhere (rt_nif.c); a supersampled frame (Opts spp > 1, which the reference
+%% does not have) is floats everywhere.
 %%
 %% Result delivery (the reference's master sends one W*H list, :116-118, :155): the frame
 %% comes back once as a binary (render_frame/5); the list is then built from the end in
@@ -31,7 +32,7 @@
          render_binary/4,
          go/4]).
 
--define(CHUNK, 16384).
+-define(CHUNK, 4096). % <= rt_nif.c PIXELS_CHUNK_MAX: one chunk stays within a NIF timeslice
 
 %% the new strategy: one GPU render, pixels keyed X+Y*Width in row-major order
 raytraced_pixel_list_gpu(Width, Height, Scene, Recursion_depth) ->

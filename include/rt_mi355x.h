@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* ---- return codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -114,7 +114,13 @@ typedef struct rt_opts {
                              device first_dev + s % ndev, so more shards than devices runs the
                              distributed strategy's split (raytracer.erl:121-149) on fewer GPUs */
     uint64_t seed;        /* jitter seed for spp > 1 */
+    /* appended in ABI 4 */
+    uint32_t flags;       /* RT_LEVELS_HIT: out_levels gets 1 where the pixel's primary ray hits an
+                             object (depth > 0), 0 elsewhere, instead of the chain's level count —
+                             all a host needs for the reference's integer {0,0,0} pixels, and it keeps
+                             the fused shading kernels that a full level count turns off */
 } rt_opts;
+#define RT_LEVELS_HIT 1
 
 /* RT_SUPERSAMPLING — stochastic supersampling (BASELINE.json config 5; the reference has
  * none, so this definition is the contract and the oracle restates it).  With spp > 1,
@@ -232,6 +238,12 @@ int rt_release(rt_prepared *p);
  *   to check that (it is many times slower). */
 #define RT_CFG_CULL 3
 int rt_configure(rt_prepared *p, int option, int64_t value);
+/* Which engine rt_launch_spp runs for this context's scene at `spp` samples per pixel:
+ * RT_ENGINE_WAVE (the wavefront kernels) or RT_ENGINE_FUSED (k_render, one kernel per frame);
+ * negative on a bad argument.  bench.py names the dominant kernel from it. */
+#define RT_ENGINE_WAVE 0
+#define RT_ENGINE_FUSED 1
+int rt_engine(rt_prepared *p, uint32_t spp);
 int rt_kernel_time(rt_prepared *p, int kernel, double *total_ms, uint64_t *launches, int reset);
 /* ---- compact slab transfer (the multi-GPU gather; raytracer.erl:151-161 collects pixels) --
  * A slab (as rt_launch writes it) is mostly background pixels, +0.0 in all three channels.

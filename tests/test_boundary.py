@@ -41,7 +41,7 @@ def test_library_targets_gfx950():
 
 def test_abi_version_and_errors(native):
     L = native.lib()
-    assert L.rt_abi_version() == 3
+    assert L.rt_abi_version() == 4
     for code in (N.RT_OK, N.RT_DONE, N.RT_EBADARG, N.RT_ENODEV, N.RT_EHIP, N.RT_ENOMEM, N.RT_ETOOBIG):
         assert N.strerror(code) and N.strerror(code) != "unknown error"
     assert N.strerror(-99) == "unknown error"

@@ -92,8 +92,30 @@ def _split_args(s):
 def test_nif_abi_checks_and_term_rule():
     c = _read("c_src", "rt_nif.c")
     assert "rt_abi_version() == RT_ABI_VERSION" in c
-    # the integer-zero rule of tests/test_oracle.py::_int_zero_rule
-    assert "if (!lights || lv.data[i] == 0)" in c
+    # the integer-zero rule of tests/test_oracle.py::_int_zero_rule (by the primary-hit mask;
+    # none at spp > 1: a supersampled frame is an average of jittered samples, always floats)
+    assert "if (!floats && (!by_hit || lv.data[i] == 0))" in c
+    assert "spp > 1 ? atom_floats : lights ? atom_true : atom_false" in c
+    assert "o.flags = RT_LEVELS_HIT" in c
     # the NIF's dirty calls are the ones that block on the GPU
     for fn in ("render_frame", "render_binary", "render_ppm_file"):
         assert re.search(rf'\{{"{fn}", \d, \w+, ERL_NIF_DIRTY_JOB_IO_BOUND\}}', c), fn
+
+
+def test_pixels_chunk_is_bounded_and_yields():
+    """pixels_chunk runs on a normal scheduler: its work per call is bounded (Count <=
+    PIXELS_CHUNK_MAX, badarg beyond), it reports its timeslice use, and raytracer_gpu's chunk is
+    within that bound (raytracer.erl's master delivers the list, :116-118, :155)."""
+    c = _read("c_src", "rt_nif.c")
+    m = re.search(r"#define PIXELS_CHUNK_MAX (\d+)", c)
+    assert m
+    limit = int(m.group(1))
+    assert limit <= 4096
+    assert "count > PIXELS_CHUNK_MAX" in c
+    body = c[c.index("static ERL_NIF_TERM pixels_chunk_nif"):]
+    body = body[:body.index("\n}\n")]
+    assert "enif_consume_timeslice(env," in body
+    assert re.search(r'\{"pixels_chunk", 5, pixels_chunk_nif, 0\}', c)  # normal scheduler, hence the bound
+    erl = _strip_comments(_read("src", "raytracer_gpu.erl"))
+    chunk = int(re.search(r"-define\(CHUNK, (\d+)\)", erl).group(1))
+    assert 0 < chunk <= limit

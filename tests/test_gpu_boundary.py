@@ -166,3 +166,20 @@ def test_pixel_list_term_types(mk, d):
         assert all(abs(x - y) <= 1e-5 for x, y in zip(a, b)), (a, b)
     keyed = rt.raytraced_pixel_list_concurrent(w, h, scene, d)
     assert [k for k, _ in keyed] == list(range(w * h))
+
+
+@pytest.mark.parametrize("name,w,h,d,spp", [("default", 160, 120, 5, 1), ("default", 97, 61, 0, 1), ("s64", 256, 256, 5, 1),
+                                            ("s256", 128, 96, 8, 4), ("mixed", 128, 96, 5, 1)])
+def test_levels_hit_mask(name, w, h, d, spp):
+    """RT_LEVELS_HIT (rt_opts.flags): out_levels is the primary-hit mask — 1 exactly where the
+    level count is positive — and the frame is the same bits as without levels (the fused
+    wavefront kernels stay on; a level count turns them off).  The strategy funs and the NIF's
+    render_frame use it for the reference's integer {0,0,0} pixels."""
+    scene = scenes.named(name)
+    plain = render(w, h, scene, d, spp=spp, seed=7)
+    img, mask = render(w, h, scene, d, spp=spp, seed=7, levels="hit")
+    img2, lv = render(w, h, scene, d, spp=spp, seed=7, levels=True)
+    assert np.array_equal(img.view(np.int64), plain.view(np.int64))
+    assert np.array_equal(img2.view(np.int64), plain.view(np.int64))
+    assert set(np.unique(mask).tolist()) <= {0, 1}
+    assert np.array_equal(mask, (lv > 0).astype(np.uint8))
