@@ -104,6 +104,12 @@ struct SceneHdr {
     // nodes and the sphere rows (o_sph) staged there (l_bvh = -1: read from HBM) and of each
     // lane's stack (l_stack).
     int bvh_ok, o_bvh, n_bvh, bvh_level, bvh_depth, l_bvh, l_bsph, l_stack;
+    // Range checks of normalize3 (rt_render.hip) proven unnecessary on the host for this scene:
+    // norm_ok — spheres only, within CULL_EXTENT, every |radius| >= 1e-50 and every light off every
+    // sphere's surface (| |L - c| - |r| | > 1e-9 (ext + 1)): the surface normals (hit - c) and the
+    // light directions (L - hit) have squared lengths inside [2^-400, 2^400]; prim_ok — the same
+    // for the primary rays' (Through - From) vectors.
+    int norm_ok, prim_ok;
     // camera (point_on_screen/3, :486-503, with focal_length/2 :483-484 folded in)
     double cam_x, cam_y, cam_z; // Camera#camera.location
     double sx;   // 0*F + Lx            (first fold step, x)

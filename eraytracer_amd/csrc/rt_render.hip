@@ -105,16 +105,22 @@ __device__ __forceinline__ double div_n(double a, double b) {
     return __builtin_fma(r, y, q);
 }
 
+// FAST: the caller guarantees x is in range (a sphere test's discriminant, >= 0.001 or 1.0 by
+// then, in a spheres-only scene within CULL_EXTENT: every ray is a unit vector — primary rays and
+// shadow rays are normalised, reflections off spheres keep the length — so disc <= ~1e10, far
+// below 2^1000), and the check is skipped.
+template <bool FAST = false>
 __device__ __forceinline__ double sqrt_x(double x) { // == sqrt(x)
     // (the fast sequence inside the wave-uniform branch: measured 3-6 % faster per frame than
     // computing it unconditionally and redoing out-of-range waves)
-    if (__ballot(!(x >= SQRT_N_LO && x <= SQRT_N_HI)) == 0) return sqrt_n(x);
+    if (FAST || __ballot(!(x >= SQRT_N_LO && x <= SQRT_N_HI)) == 0) return sqrt_n(x);
     return sqrt(x);
 }
 
-__device__ __forceinline__ D3 normalize3(const D3 &v) { // vector_normalize/1 (:554-560)
+// fast (wave-uniform): the host proved m2 inside the range (SceneHdr::norm_ok / prim_ok)
+__device__ __forceinline__ D3 normalize3(const D3 &v, bool fast = false) { // vector_normalize/1 (:554-560)
     const double m2 = v.x * v.x + v.y * v.y + v.z * v.z;
-    if (__ballot(!(m2 >= RCP_N_LO && m2 <= RCP_N_HI)) == 0) { // mag and 1/mag in range, mag != 0
+    if (fast || __ballot(!(m2 >= RCP_N_LO && m2 <= RCP_N_HI)) == 0) { // mag and 1/mag in range, mag != 0
         const double s = div_n(1.0, sqrt_n(m2));
         return D3{v.x * s, v.y * s, v.z * s};
     }
@@ -175,10 +181,11 @@ __device__ __forceinline__ double pow_libm(double x, double y) {
 
 // ---- primitive tests: return true and t on a valid hit --------------------------------------
 // ray_sphere_intersect/2 (:364-397), from B and C (A4 = 4*A hoisted per ray)
+template <bool FAST = false>
 __device__ __forceinline__ bool sph_t(double B, double C, double A4, double &t) {
     double disc = B * B - A4 * C;
     if (!(disc >= 0.001)) return false;
-    double sq = sqrt_x(disc);
+    double sq = sqrt_x<FAST>(disc);
     double t0 = (-B + sq) / 2;
     double t1 = (-B - sq) / 2;
     if (!((t0 >= 0) && (t1 >= 0))) return false;
@@ -211,12 +218,13 @@ __device__ __forceinline__ bool pl_t(const D3 &n, const D3 &d, double V0, double
 
 // The same decision as sph_t without divergent branches: the root computation runs for the
 // whole wave unless no lane can hit (a wave-uniform test), and the outcome is a mask.
+template <bool FAST = false>
 __device__ __forceinline__ bool sph_t_wave(double B, double C, double A4, double &t) {
     const double disc = B * B - A4 * C;
     const bool ok = disc >= 0.001;
     t = 0.0;
     if (__ballot(ok) == 0) return false;
-    const double sq = sqrt_x(ok ? disc : 1.0);
+    const double sq = sqrt_x<FAST>(ok ? disc : 1.0);
     const double t0 = (-B + sq) / 2;
     const double t1 = (-B - sq) / 2;
     t = (t1 < t0) ? t1 : t0;
@@ -498,12 +506,14 @@ __device__ __forceinline__ Beam32 make_beam32(const SceneHdr &h, bool act, const
     constexpr float DIR_TOL = 1.0e-6f;
     const float dd = dx * dx + dy * dy + dz * dz;
     const float cl = ax * dx + ay * dy + az * dz;
-    const float qx = ay * dz - az * dy, qy = az * dx - ax * dz, qz = ax * dy - ay * dx;
-    const float sl = __builtin_sqrtf(qx * qx + qy * qy + qz * qz);
     const bool bad = act && !(dd > 1.0f - 0.5f * DIR_TOL && dd < 1.0f + 0.5f * DIR_TOL);
-    const float c = wave_reduce32(act ? cl : 2.0f, [](float x, float y) { return fminf(x, y); }) - BEAM32_EPS - 2 * DIR_TOL;
-    const float s = wave_reduce32(act ? sl : 0.0f, [](float x, float y) { return fmaxf(x, y); }) + BEAM32_EPS + 2 * DIR_TOL;
+    const float cmin = wave_reduce32(act ? cl : 2.0f, [](float x, float y) { return fminf(x, y); });
+    const float c = cmin - BEAM32_EPS - 2 * DIR_TOL;
     if (__ballot(bad) != 0 || !(c > 0.0f)) return b; // cone wider than a hemisphere: scan everything
+    // The sine bound from the cosine bound: every lane has cos >= cmin (to f32 rounding, ~1e-6 with
+    // the directions' and the axis' deviation from unit length), so sin^2 = |a|^2 |d|^2 - cos^2 <=
+    // 1 + 4 DIR_TOL - cmin^2 (0 < cmin <= 1) — no second reduction (nor the lanes' cross products).
+    const float s = __builtin_sqrtf(fmaxf(1.0f + 4 * DIR_TOL - cmin * cmin, 0.0f)) + BEAM32_EPS + 2 * DIR_TOL;
     const int first = __builtin_ctzll(am);
     const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
     b.mx = lane_f32(ox, first);
@@ -511,10 +521,13 @@ __device__ __forceinline__ Beam32 make_beam32(const SceneHdr &h, bool act, const
     b.mz = lane_f32(oz, first);
     const float ex = ox - b.mx, ey = oy - b.my, ez = oz - b.mz;
     const float r2 = wave_reduce32(act ? ex * ex + ey * ey + ez * ez : 0.0f, [](float x, float y) { return fmaxf(x, y); });
-    const double mo = wave_max(act ? fmax(fabs(o.x), fmax(fabs(o.y), fabs(o.z))) : 0.0);
-    if (!(mo <= CULL_EXTENT)) return b;
+    // the origins' extent in binary32 (|o| rounded to nearest: within 2^-24 relative, far inside the
+    // 1e-6 margin below; the extent check keeps a 1e-6 relative slack for it)
+    const float mo = wave_reduce32(act ? fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz))) : 0.0f,
+                                   [](float x, float y) { return fmaxf(x, y); });
+    if (!(mo <= (float)(CULL_EXTENT * (1.0 - 1.0e-6)))) return b;
     b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
-    b.ro = __builtin_sqrtf(r2) * (1.0f + BEAM32_EPS) + BEAM32_EPS + (float)((mo + h.ext) * 1.0e-6);
+    b.ro = __builtin_sqrtf(r2) * (1.0f + BEAM32_EPS) + BEAM32_EPS + (mo + (float)h.ext) * 1.0e-6f;
     b.on = true;
     return b;
 }
@@ -581,22 +594,18 @@ __device__ __forceinline__ Beam32 make_beam_pair32(const SceneHdr &h, bool a0, c
     const float inv = __builtin_amdgcn_rsqf(n2);
     const float ax = rx * inv, ay = ry * inv, az = rz * inv;
     constexpr float DIR_TOL = 1.0e-6f; // as in make_beam32
-    auto lane_terms = [&](bool a, float dx, float dy, float dz, float &cl, float &q2) {
+    auto lane_terms = [&](bool a, float dx, float dy, float dz, float &cl) {
         const float dd = dx * dx + dy * dy + dz * dz;
         cl = ax * dx + ay * dy + az * dz;
-        const float qx = ay * dz - az * dy, qy = az * dx - ax * dz, qz = ax * dy - ay * dx;
-        q2 = qx * qx + qy * qy + qz * qz;
         return a && !(dd > 1.0f - 0.5f * DIR_TOL && dd < 1.0f + 0.5f * DIR_TOL);
     };
-    float cl0, q20, cl1, q21;
-    const bool bad0 = lane_terms(a0, x0, y0, z0, cl0, q20); // both sets evaluated (no short circuit)
-    const bool bad1 = lane_terms(a1, x1, y1, z1, cl1, q21);
-    const float cmin = fminf(a0 ? cl0 : 2.0f, a1 ? cl1 : 2.0f);
-    const float q2max = fmaxf(a0 ? q20 : 0.0f, a1 ? q21 : 0.0f);
-    const float c = wave_reduce32(cmin, [](float x, float y) { return fminf(x, y); }) - BEAM32_EPS - 2 * DIR_TOL;
-    const float s = __builtin_sqrtf(wave_reduce32(q2max, [](float x, float y) { return fmaxf(x, y); })) * (1.0f + BEAM32_EPS) +
-                    BEAM32_EPS + 2 * DIR_TOL;
+    float cl0, cl1;
+    const bool bad0 = lane_terms(a0, x0, y0, z0, cl0); // both sets evaluated (no short circuit)
+    const bool bad1 = lane_terms(a1, x1, y1, z1, cl1);
+    const float cmin = wave_reduce32(fminf(a0 ? cl0 : 2.0f, a1 ? cl1 : 2.0f), [](float x, float y) { return fminf(x, y); });
+    const float c = cmin - BEAM32_EPS - 2 * DIR_TOL;
     if (__ballot(bad0 || bad1) != 0 || !(c > 0.0f)) return b;
+    const float s = __builtin_sqrtf(fmaxf(1.0f + 4 * DIR_TOL - cmin * cmin, 0.0f)) + BEAM32_EPS + 2 * DIR_TOL; // make_beam32
     b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
     b.on = true;
     return b;
@@ -627,7 +636,7 @@ __device__ __forceinline__ void sphere_BC(const Scene &S, int org, const D3 &o, 
     }
 }
 // ILP = false: one candidate per step (the least work: dense, throughput-bound waves).
-template <bool PRE, bool ILP = false>
+template <bool PRE, bool ILP = false, bool FAST = false>
 __device__ __forceinline__ void scan_spheres(const Scene &S, int org, const D3 &o, const D3 &d, double A4, int chunk,
                                              unsigned long long m, double &bt, int &bid) {
     const SceneHdr &h = S.h;
@@ -639,7 +648,7 @@ __device__ __forceinline__ void scan_spheres(const Scene &S, int org, const D3 &
         sphere_BC<PRE>(S, org, o, d, k, B, C);
         const int id = S.itab[h.i_sph_id + k];
         double t;
-        const bool upd = (int)sph_t_wave(B, C, A4, t) & (int)nearer(t, id, bt, bid);
+        const bool upd = (int)sph_t_wave<FAST>(B, C, A4, t) & (int)nearer(t, id, bt, bid);
         bt = upd ? t : bt;
         bid = upd ? id : bid;
     }
@@ -657,7 +666,7 @@ __device__ __forceinline__ void scan_spheres(const Scene &S, int org, const D3 &
         const double disc0 = B0 * B0 - A4 * C0, disc1 = B1 * B1 - A4 * C1;
         const bool ok0 = disc0 >= 0.001, ok1 = disc1 >= 0.001;
         if (__ballot(ok0 | ok1) == 0) continue;
-        const double sq0 = sqrt_x(ok0 ? disc0 : 1.0), sq1 = sqrt_x(ok1 ? disc1 : 1.0);
+        const double sq0 = sqrt_x<FAST>(ok0 ? disc0 : 1.0), sq1 = sqrt_x<FAST>(ok1 ? disc1 : 1.0);
         const double a0 = (-B0 + sq0) / 2, b0 = (-B0 - sq0) / 2;
         const double a1 = (-B1 + sq1) / 2, b1 = (-B1 - sq1) / 2;
         const double t0 = (b0 < a0) ? b0 : a0, t1 = (b1 < a1) ? b1 : a1;
@@ -775,7 +784,7 @@ __device__ __forceinline__ void stage_bvh(const Scene &S) {
 }
 // LDS: the nodes are staged in LDS (h.l_bvh >= 0), ROWS: the sphere rows too (h.l_bsph >= 0);
 // else read from HBM (L2)
-template <bool LDS, bool ROWS>
+template <bool LDS, bool ROWS, bool FAST = false>
 __device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &d, double A4, bool act, double &bt,
                                          int &bid) {
     const SceneHdr &h = S.h;
@@ -797,7 +806,7 @@ __device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &
         const double B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
         const double C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - c2r.y;
         double t;
-        if (sph_t(B, C, A4, t) && nearer(t, id, bt, bid)) {
+        if (sph_t<FAST>(B, C, A4, t) && nearer(t, id, bt, bid)) {
             bt = t;
             bid = id;
             tlim = (float)t * HI;
@@ -858,11 +867,11 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
     RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
     if (!PRE && bvh) { // (wave-uniform) per-lane BVH traversal, then the triangles and planes
         if (h.l_bvh >= 0 && h.l_bsph >= 0)
-            scan_bvh<true, true>(S, o, d, A4, act, bt, bid);
+            scan_bvh<true, true, (SPH >= 1)>(S, o, d, A4, act, bt, bid);
         else if (h.l_bvh >= 0)
-            scan_bvh<true, false>(S, o, d, A4, act, bt, bid);
+            scan_bvh<true, false, (SPH >= 1)>(S, o, d, A4, act, bt, bid);
         else
-            scan_bvh<false, false>(S, o, d, A4, act, bt, bid);
+            scan_bvh<false, false, (SPH >= 1)>(S, o, d, A4, act, bt, bid);
         scan_tri_pl<PRE>(S, org, o, d, bt, bid);
         return (act && bid != 0x7fffffff) ? bid : -1;
     }
@@ -892,7 +901,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
         }
 #pragma unroll
         for (int c = 0; c < UCH; ++c)
-            if (c < nch) scan_spheres<false, ILP>(S, org, o, d, A4, c * 64, all ? chunk_all(h.n_sph, c * 64) : m[c], bt, bid);
+            if (c < nch) scan_spheres<false, ILP, (SPH >= 1)>(S, org, o, d, A4, c * 64, all ? chunk_all(h.n_sph, c * 64) : m[c], bt, bid);
         rem = 0;
     }
     for (int g = 0; g < MAX_GROUPS && rem; ++g) {
@@ -909,7 +918,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
             RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
             for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
                 const unsigned long long m = b.on ? cull_chunk<SPH>(S, b, chunk, org) : chunk_all(h.n_sph, chunk);
-                scan_spheres<PRE, ILP>(S, org, o, d, A4, chunk, m, bt, bid);
+                scan_spheres<PRE, ILP, (SPH >= 1)>(S, org, o, d, A4, chunk, m, bt, bid);
             }
         } else {
             const Beam32 b = make_beam32(h, sel, o, d);
@@ -917,7 +926,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
             RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
             for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
                 const unsigned long long m = b.on ? cull_chunk32<SPH>(S, b, chunk) : chunk_all(h.n_sph, chunk);
-                scan_spheres<PRE, ILP>(S, org, o, d, A4, chunk, m, bt, bid);
+                scan_spheres<PRE, ILP, (SPH >= 1)>(S, org, o, d, A4, chunk, m, bt, bid);
             }
         }
         if (!on) break; // everything was scanned
@@ -929,6 +938,9 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
 // nearest_object_intersecting_ray/6 for two rays per lane from tabled origin `org` (primary
 // rays): one beam and one candidate walk serve both, and each candidate's two tests are
 // independent (instruction-level parallelism for the wave).
+// FAST: the scene's spheres and the camera are within CULL_EXTENT (unit primary rays: every
+// discriminant in sqrt_x's range, see there).
+template <bool FAST>
 __device__ __forceinline__ void nearest_pair(const Scene &S, int org, const D3 &o, const D3 &d0, const D3 &d1, bool a0,
                                              bool a1, int &id0, double &t0, int &id1, double &t1) {
     const SceneHdr &h = S.h;
@@ -951,8 +963,8 @@ __device__ __forceinline__ void nearest_pair(const Scene &S, int org, const D3 &
             const double qx = q[0], qy = q[1], qz = q[2], C = q[3];
             const int id = S.itab[h.i_sph_id + k];
             double u0, u1;
-            const bool h0 = sph_t_wave(2 * (d0.x * qx + d0.y * qy + d0.z * qz), C, A40, u0);
-            const bool h1 = sph_t_wave(2 * (d1.x * qx + d1.y * qy + d1.z * qz), C, A41, u1);
+            const bool h0 = sph_t_wave<FAST>(2 * (d0.x * qx + d0.y * qy + d0.z * qz), C, A40, u0);
+            const bool h1 = sph_t_wave<FAST>(2 * (d1.x * qx + d1.y * qy + d1.z * qz), C, A41, u1);
             const bool up0 = h0 & nearer(u0, id, bt0, bid0), up1 = h1 & nearer(u1, id, bt1, bid1);
             bt0 = up0 ? u0 : bt0; bid0 = up0 ? id : bid0;
             bt1 = up1 ? u1 : bt1; bid1 = up1 ? id : bid1;
@@ -1092,7 +1104,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
         if (SPH || kind == K_SPHERE) {
             const double *q = org_row<SPH>(S, org, loc);
             double B = 2 * (sd.x * q[0] + sd.y * q[1] + sd.z * q[2]);
-            valid = sph_t(B, q[3], A4, ts);
+            valid = SPH ? sph_t<true>(B, q[3], A4, ts) : sph_t(B, q[3], A4, ts);
             if (SPH != 2 && h.occ_cells > 1) cell = occ_cell(q, sd); // (staged scenes: one cell)
         } else if (kind == K_TRIANGLE) {
             const double *g = S.tab + h.o_tri + loc * TRI_W;
@@ -1136,7 +1148,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
                 const int id = sph_id<SPH>(S, k);
                 const double B = 2 * (sd.x * q01.x + sd.y * q01.y + sd.z * q23.x);
                 double t;
-                const bool hit = sph_t_wave(B, q23.y, A4, t);
+                const bool hit = sph_t_wave<(SPH >= 1)>(B, q23.y, A4, t);
                 blocked = blocked | (w & hit & ((t < ts) | ((t == ts) & (id < c))));
             }
             if (__all(blocked)) return false;
@@ -1214,7 +1226,7 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
         const D3 mc = {m[3], m34.x, m34.y};
         const double spow = m67.x, shin = m67.y;
         // diffuse_term/4 (:272-279)
-        const D3 ln = normalize3(D3{Lp.x - hit.x, Lp.y - hit.y, Lp.z - hit.z});
+        const D3 ln = normalize3(D3{Lp.x - hit.x, Lp.y - hit.y, Lp.z - hit.z}, SPH && h.norm_ok);
         const double dd = max0(dot3(N, ln));
         const D3 diff = {mc.x * dd, mc.y * dd, mc.z * dd};
         // specular_term/7 (:285-297)
@@ -1265,7 +1277,7 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
     const double px = 0.0 + ((X - 0.5) * hdr.screen_w + hdr.sx);
     const double py = (Y - 0.5) * hdr.screen_h + hdr.sy;
     const D3 cam = {hdr.cam_x, hdr.cam_y, hdr.cam_z};
-    const D3 d0 = normalize3(D3{px - hdr.cam_x, py - hdr.cam_y, hdr.dz});
+    const D3 d0 = normalize3(D3{px - hdr.cam_x, py - hdr.cam_y, hdr.dz}, hdr.prim_ok);
 
     D3 col = {0.0, 0.0, 0.0};
     int nlev = 0;
@@ -1470,8 +1482,8 @@ struct DevGuard { // restore the caller's current device on scope exit
 };
 
 // RT_CFG_CULL = 0: every scan tests every object (no wave beams or cones, no occluder masks, no
-// BVH, no LDS-staged tables) — the reference's brute-force scans, against which the filters'
-// frames are checked bit for bit (tests/test_gpu_frames.py).
+// BVH, no LDS-staged tables, no host-proven skips of range checks) — the reference's brute-force
+// scans, against which the filters' frames are checked bit for bit (tests/test_gpu_frames.py).
 void apply_cull(rt_prepared *p) {
     p->hdr = p->hdr_full;
     if (!p->cull) {
@@ -1479,6 +1491,8 @@ void apply_cull(rt_prepared *p) {
         p->hdr.beam_ok = 0;
         p->hdr.bvh_ok = 0;
         p->hdr.l_bytes = 0;
+        p->hdr.norm_ok = 0; // and every range check of normalize3 on
+        p->hdr.prim_ok = 0;
     }
 }
 

@@ -518,6 +518,23 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
         h.cull_ok = ext <= CULL_EXTENT ? 1 : 0;
         h.ext = ext;
     }
+    {
+        // normalize3's range checks that cannot fail (SceneHdr::norm_ok / prim_ok)
+        bool ok = h.cull_ok && h.n_tri == 0 && h.n_pl == 0;
+        const double tol = 1.0e-9 * (h.ext + 1.0);
+        for (int i : sph) {
+            if (!ok) break;
+            const auto &s = e[i].u.sphere;
+            const double r = std::fabs(s.radius);
+            if (!(r >= 1.0e-50)) ok = false;
+            for (int li : lights) {
+                const rt_vec3 &L = e[li].u.point_light.location;
+                const double dx = L.x - s.center.x, dy = L.y - s.center.y, dz = L.z - s.center.z;
+                if (!(std::fabs(std::sqrt(dx * dx + dy * dy + dz * dz) - r) > tol)) ok = false;
+            }
+        }
+        h.norm_ok = ok ? 1 : 0;
+    }
     // Wave beams (a cone over the wave's rays, a candidate mask per 64 spheres) cost a few wave
     // reductions per scan; with a handful of spheres testing every one is cheaper
     // (RT_BEAM_MIN overrides the threshold, for A/B runs).
@@ -665,6 +682,14 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
     h.screen_w = SW;
     h.screen_h = SH;
     h.n_light_d = (double)h.n_light;
+    {
+        // primary rays: Through - From = (px - cx, py - cy, dz) with X, Y in [0, 1]: squared length
+        // at least dz^2, at most (|sx| + |w| + |cx|)^2 + (|sy| + |h| + |cy|)^2 + dz^2 (prim_ok)
+        const double bx = std::fabs(h.sx) + std::fabs(h.screen_w) + std::fabs(h.cam_x);
+        const double by = std::fabs(h.sy) + std::fabs(h.screen_h) + std::fabs(h.cam_y);
+        const double lo = h.dz * h.dz, hi = bx * bx + by * by + h.dz * h.dz;
+        h.prim_ok = (lo >= 1.0e-100 && hi <= 1.0e100) ? 1 : 0;
+    }
     // LDS staging layout (16-byte aligned sections)
     h.l_obj = h.l_meta = h.l_org = h.l_occ = h.l_id = h.l_sphb = -1;
     h.l_bytes = 0;
