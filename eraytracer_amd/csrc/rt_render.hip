@@ -1927,7 +1927,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
         const PassGeom g{W, H, rb, sh, ns, row0, spp, sample, seed, acc_p}; // level-0 records are rebuilt from it
-        dim3 grid(tiles_x, (rows + TILE - 1) / TILE);
+        const dim3 grid(std::min(ntiles, PRIMARY_GRID)); // k_primary: grid-stride loop over the tiles
         {
             KtScope kt(p, RT_KT_PRIMARY, st);
             if (lv0)
