@@ -940,9 +940,12 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
 // independent (instruction-level parallelism for the wave).
 // FAST: the scene's spheres and the camera are within CULL_EXTENT (unit primary rays: every
 // discriminant in sqrt_x's range, see there).
+// pm (wave-uniform, or null): this wave's candidate masks, one per 64-sphere chunk, precomputed
+// for its 8x16 pixel block (k_pmask) — then no beam is built here.
 template <bool FAST>
 __device__ __forceinline__ void nearest_pair(const Scene &S, int org, const D3 &o, const D3 &d0, const D3 &d1, bool a0,
-                                             bool a1, int &id0, double &t0, int &id1, double &t1) {
+                                             bool a1, int &id0, double &t0, int &id1, double &t1,
+                                             const unsigned long long *pm = nullptr) {
     const SceneHdr &h = S.h;
     double bt0 = __builtin_inf(), bt1 = __builtin_inf();
     int bid0 = 0x7fffffff, bid1 = 0x7fffffff;
@@ -951,10 +954,12 @@ __device__ __forceinline__ void nearest_pair(const Scene &S, int org, const D3 &
     if (__ballot(a0 | a1) == 0) return;
     const double A40 = 4 * (d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
     const double A41 = 4 * (d1.x * d1.x + d1.y * d1.y + d1.z * d1.z);
-    const Beam32 b = make_beam_pair32(h, a0, d0, a1, d1);
+    Beam32 b;
+    b.on = false;
+    if (!pm) b = make_beam_pair32(h, a0, d0, a1, d1);
     RT_STAT(ST_NEAR_PRE, 1);
     for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
-        unsigned long long m = b.on ? cull_chunk32_org(S, b, chunk, org) : chunk_all(h.n_sph, chunk);
+        unsigned long long m = pm ? pm[chunk >> 6] : b.on ? cull_chunk32_org(S, b, chunk, org) : chunk_all(h.n_sph, chunk);
         RT_STAT(ST_NEAR_PRE_CAND, __popcll(m));
         while (m) {
             const int k = chunk + __builtin_ctzll(m);
@@ -1430,6 +1435,12 @@ struct rt_prepared {
     size_t counts_bytes = 0;
     int *d_items = nullptr;   // per-level record counts, then per-level dense slot lists
     size_t items_bytes = 0;
+    // primary rays' candidate masks per 8x16 pixel block of the slab (k_pmask), kept while the
+    // frame geometry and the scene stay the same
+    unsigned long long *d_pmask = nullptr;
+    size_t pmask_bytes = 0;
+    long long pmask_key[8] = {};
+    bool pmask_valid = false;
     // the shadow pass runs on a second, low-priority stream beside the reflection chain
     // shading of level 0 and of the deeper levels.  The caller's stream plus these stay
     // within the hardware queues a process gets by default (GPU_MAX_HW_QUEUES=4): streams
@@ -1745,6 +1756,7 @@ int rt_release(rt_prepared *p) {
     if (p->d_sample) (void)hipFree(p->d_sample);
     if (p->d_counts) (void)hipFree(p->d_counts);
     if (p->d_items) (void)hipFree(p->d_items);
+    if (p->d_pmask) (void)hipFree(p->d_pmask);
     for (hipEvent_t &e : p->ev_level)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t &e : p->ev_lit)
@@ -1810,6 +1822,16 @@ int grow(void **buf, size_t *have, size_t need, unsigned *gen) {
     return RT_OK;
 }
 
+// Primary rays' candidate masks precomputed per frame geometry (k_pmask); RT_PMASK=0 builds the
+// beams in k_primary every frame, for A/B runs.
+bool pmask_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("RT_PMASK");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
 // Each level's shading fused into the next reflection pass (k_reflect_shade) when the context runs
 // without side streams; RT_FUSE_SHADE=0 keeps separate k_light launches, for A/B runs.
 bool fuse_on() {
@@ -1867,6 +1889,32 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     const bool overlap = lit_overlap(p) && D > 1 && p->hdr.n_light > 0;
     if (rc == RT_OK && overlap) rc = side_stream(p);
     if (rc != RT_OK) return rc;
+    // the primary rays' candidate masks of the whole slab (k_pmask), recomputed only when the
+    // frame geometry, the scene or the work space (gen) changed
+    const unsigned long long *pmask = nullptr;
+    if (p->hdr.beam_ok && D > 0 && pmask_on()) {
+        const int slab_all = (int)rt_shard_rows(H, rb, ns);
+        const size_t nhalf = (size_t)tiles_x * ((slab_all + TILE - 1) / TILE) * 2;
+        const long long key[8] = {W, H, rb, sh, ns, spp > 1, (long long)p->gen, slab_all};
+        if (!(p->pmask_valid && std::memcmp(key, p->pmask_key, sizeof(key)) == 0)) {
+            p->pmask_valid = false;
+            unsigned dummy = 0; // (not part of the captured work space: gen untouched)
+            if ((rc = grow(reinterpret_cast<void **>(&p->d_pmask), &p->pmask_bytes, nhalf * p->hdr.n_chunk * 8, &dummy)) !=
+                RT_OK)
+                return rc;
+            const dim3 pg((unsigned)std::min<size_t>(4096, (nhalf + 3) / 4));
+            if (spp > 1)
+                hipLaunchKernelGGL(k_pmask<true>, pg, dim3(256), 0, st, p->hdr, p->d_tab, p->d_itab, W, H, rb, sh, ns,
+                                   slab_all, (int)nhalf, p->d_pmask);
+            else
+                hipLaunchKernelGGL(k_pmask<false>, pg, dim3(256), 0, st, p->hdr, p->d_tab, p->d_itab, W, H, rb, sh, ns,
+                                   slab_all, (int)nhalf, p->d_pmask);
+            HIPCHK(hipGetLastError());
+            std::memcpy(p->pmask_key, key, sizeof(key));
+            p->pmask_valid = true;
+        }
+        pmask = p->d_pmask;
+    }
     // streams of the shading pass: level 0 (the bulk) beside the whole reflection chain, the
     // next levels each on their own, so no level waits for another's shading
     auto ls = [&](int k) { return overlap ? p->side[std::min(k, 1)] : st; };
@@ -1932,10 +1980,12 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             KtScope kt(p, RT_KT_PRIMARY, st);
             if (lv0)
                 hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W,
-                                   H, D, rb, sh, ns, rows, row0, o, lv0, q, p->d_counts, ntiles, spp, sample, seed, acc_p);
+                                   H, D, rb, sh, ns, rows, row0, o, lv0, q, p->d_counts, ntiles, spp, sample, seed, acc_p,
+                                   pmask);
             else
                 hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
-                                   W, H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed, acc_p);
+                                   W, H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed, acc_p,
+                                   pmask);
         }
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
