@@ -1084,6 +1084,14 @@ __device__ __forceinline__ int occ_cell(const double *q, const D3 &sd) {
     const int drop = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
     const float ex = (float)sd.x * D + qx, ey = (float)sd.y * D + qy, ez = (float)sd.z * D + qz;
     const float ei = drop == 0 ? ey : ex, ej = drop == 2 ? ey : ez;
+    if (OCC_CELLS == 64) { // per axis: the sign and |e| against r/4, r/2, 3r/4 (8 bins), cell = bi + 8 bj
+        const float t2 = (float)(((q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) - q[3]) * 0.25); // (r/2)^2
+        auto bin = [&](float e) {
+            const float e2 = e * e;
+            return (e >= 0.0f ? 4 : 0) + (e2 >= 0.25f * t2 ? 1 : 0) + (e2 >= t2 ? 1 : 0) + (e2 >= 2.25f * t2 ? 1 : 0);
+        };
+        return bin(ei) + 8 * bin(ej);
+    }
     int cell = (ei >= 0.0f ? 1 : 0) + (ej >= 0.0f ? 2 : 0);
     if (OCC_CELLS == 16) {
         const float t2 = (float)(((q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) - q[3]) * 0.25); // (r/2)^2

@@ -640,20 +640,40 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
                     // the cone of sphere j reaches s*(dir_k - a_k) in [lo, hi] (widened by eps):
                     // its largest s*dir_k is cos(max(0, psi - rho)), its smallest cos(min(pi, psi + rho))
                     const double eps = OCC_CELL_EPS, tau = rt / D * 0.5; // the kernel's |sd - a| split
-                    auto reach = [&](int k, double s, bool outer, bool split) {
+                    // does the cone reach s*(dir_k - a_k) in [t_lo, t_hi]?
+                    auto reach = [&](int k, double s, double t_lo, double t_hi) {
                         const double psi = std::acos(std::max(-1.0, std::min(1.0, s * w3[k])));
                         const double top = psi <= rho ? 1.0 : std::cos(psi - rho);
                         const double bot = psi + rho >= M_PI ? -1.0 : std::cos(psi + rho);
-                        const double lo = split && outer ? tau - eps : -eps;
-                        if (top + 1e-7 < s * a3[k] + lo) return false;
-                        if (split && !outer && bot - 1e-7 > s * a3[k] + tau + eps) return false;
+                        if (top + 1e-7 < s * a3[k] + t_lo - eps) return false;
+                        if (bot - 1e-7 > s * a3[k] + t_hi + eps) return false;
                         return true;
                     };
+                    // the kernel's bins along one axis (occ_cell): the sign of dir_k - a_k and, with
+                    // 16 cells, |dir_k - a_k| below / above tau; with 64, below tau/2, tau, 3 tau/2 or above
+                    auto bin = [&](int b, double &s, double &t_lo, double &t_hi) {
+                        const double inf = 1e300;
+                        if (ncell == 4) {
+                            s = (b & 1) ? 1.0 : -1.0; t_lo = 0; t_hi = inf;
+                        } else if (ncell == 16) {
+                            s = (b & 1) ? 1.0 : -1.0;
+                            t_lo = (b & 2) ? tau : 0.0; t_hi = (b & 2) ? inf : tau;
+                        } else {
+                            s = (b & 4) ? 1.0 : -1.0;
+                            const int g = b & 3;
+                            t_lo = g * 0.5 * tau; t_hi = g == 3 ? inf : (g + 1) * 0.5 * tau;
+                        }
+                    };
                     for (int c = 0; c < ncell; c++) {
-                        const double si = (c & 1) ? 1.0 : -1.0, sj = (c & 2) ? 1.0 : -1.0;
-                        const bool split = ncell == 16;
-                        if (!cells || ncell == 1 ||
-                            (reach(axi, si, (c & 4) != 0, split) && reach(axj, sj, (c & 8) != 0, split)))
+                        // cell -> the bins of axes i and j (occ_cell's numbering)
+                        int bi = 0, bj = 0;
+                        if (ncell == 4) { bi = c & 1; bj = (c >> 1) & 1; }
+                        else if (ncell == 16) { bi = (c & 1) | ((c >> 1) & 2); bj = ((c >> 1) & 1) | ((c >> 2) & 2); }
+                        else { bi = c & 7; bj = c >> 3; }
+                        double si, li, hi_, sj, lj, hj;
+                        bin(bi, si, li, hi_);
+                        bin(bj, sj, lj, hj);
+                        if (!cells || ncell == 1 || (reach(axi, si, li, hi_) && reach(axj, sj, lj, hj)))
                             m[(size_t)c * h.n_chunk + j / 64] |= 1ull << (j % 64);
                     }
                 }
