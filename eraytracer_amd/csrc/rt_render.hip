@@ -855,7 +855,9 @@ __device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &
 #endif
 constexpr int MAX_GROUPS = RT_MAX_GROUPS;
 constexpr int UNION_CHUNKS = 4; // reflection scans of scenes up to 256 spheres walk the union of the groups' candidates
-template <bool PRE, bool ILP = false, int SPH = 0>
+// NB: the scene has no wave beams (beam_ok = 0, host-checked): every chunk is scanned whole and
+// the beam code is compiled out (registers: the fused engine's occupancy).
+template <bool PRE, bool ILP = false, int SPH = 0, bool NB = false>
 __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, const D3 &d, double &bt, bool act,
                                        int grp = -1, bool bvh = false) {
     const SceneHdr &h = S.h;
@@ -865,6 +867,12 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
     const double A4 = 4 * (d.x * d.x + d.y * d.y + d.z * d.z);
     RT_STAT(PRE ? ST_NEAR_PRE : ST_NEAR_GEN, 1);
     RT_STAT(ST_NEAR_LANES, __popcll(__ballot(act)));
+    if constexpr (NB) {
+        for (int chunk = 0; chunk < h.n_sph; chunk += 64)
+            scan_spheres<PRE, ILP, (SPH >= 1)>(S, org, o, d, A4, chunk, chunk_all(h.n_sph, chunk), bt, bid);
+        scan_tri_pl<PRE>(S, org, o, d, bt, bid);
+        return (act && bid != 0x7fffffff) ? bid : -1;
+    }
     if (!PRE && bvh) { // (wave-uniform) per-lane BVH traversal, then the triangles and planes
         if (h.l_bvh >= 0 && h.l_bsph >= 0)
             scan_bvh<true, true, (SPH >= 1)>(S, o, d, A4, act, bt, bid);
@@ -1102,7 +1110,7 @@ __device__ __forceinline__ int occ_cell(const double *q, const D3 &sd) {
 
 // SPH: the scene holds only spheres and culling is on (host-checked), so every target is a
 // sphere with occluder masks: the cone and triangle/plane paths are compiled out (registers).
-template <int SPH = 0>
+template <int SPH = 0, bool NB = false>
 __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &T, const D3 &sd, bool active,
                                        const HitBall &hb, const D3 &Lp) {
     const SceneHdr &h = S.h;
@@ -1138,7 +1146,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
     double tmax = __builtin_inf();
     Beam b;
     b.on = false;
-    if (!SPH && !sph_targets) b = shadow_cone(hb, Lp, tmax); // shadow rays all start at the light
+    if (!SPH && !NB && !sph_targets) b = shadow_cone(hb, Lp, tmax); // shadow rays all start at the light
     RT_STAT(ST_SHADOW, 1);
     RT_STAT(ST_SHADOW_CONE_ON, (sph_targets || b.on) ? 1 : 0);
     for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
@@ -1167,7 +1175,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
             if (__all(blocked)) return false;
             continue;
         } else if (!SPH) {
-            m = b.on ? cull_chunk(S, b, chunk, org, tmax) : chunk_all(h.n_sph, chunk);
+            m = (!NB && b.on) ? cull_chunk(S, b, chunk, org, tmax) : chunk_all(h.n_sph, chunk);
             if (skip >= chunk && skip < chunk + 64) m &= ~(1ull << (skip - chunk));
         }
         RT_STAT(ST_SHADOW_CAND, __popcll(m));
@@ -1218,7 +1226,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
 // re-read per light for the same reason.
 // bits (optional): bit i set where light i's shadow test passed (lights 0..31; only lanes whose
 // light term is not exactly zero are tested, the others' bits are 0 and never matter).
-template <bool GENPOW, int SPH = 0>
+template <bool GENPOW, int SPH = 0, bool NB = false>
 __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D3 &hit, const D3 &N, const D3 &col,
                                     double refl, bool active, unsigned *bits = nullptr) {
     const SceneHdr &h = S.h;
@@ -1229,7 +1237,7 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
     HitBall hb;
     hb.on = false;
     hb.cx = hb.cy = hb.cz = hb.r = 0.0;
-    if (!SPH && __ballot(active && T.kind != K_SPHERE) != 0) hb = make_hitball(h, active, hit);
+    if (!SPH && !NB && __ballot(active && T.kind != K_SPHERE) != 0) hb = make_hitball(h, active, hit);
     RT_STAT(ST_SHADE, 1);
     D3 F = {0.0, 0.0, 0.0};
     for (int i = 0; i < h.n_light; ++i) {
@@ -1252,7 +1260,7 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
         const D3 lc = {Lc.x * con.x, Lc.y * con.y, Lc.z * con.z};
         const bool need = active && !(lc.x == 0.0 && lc.y == 0.0 && lc.z == 0.0);
         // shadow ray direction normalize(Hit - Light) == -normalize(Light - Hit), bit for bit
-        const bool lb = lit_by<SPH>(S, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp);
+        const bool lb = lit_by<SPH, NB>(S, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp);
         if (bits && lb && i < 32) *bits |= 1u << i;
         const double lit = lb ? 1.0 : 0.0;
         F.x = F.x + (col.x * refl + lc.x * lit);
@@ -1262,8 +1270,15 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
     return F;
 }
 
-template <int ORDER, int PREC, bool LEVELS, bool GENPOW>
-__global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict__ tab,
+// The beam-free build (NB) needs fewer registers: its own occupancy target.
+#ifndef RT_FUSED_NB_WAVES
+#define RT_FUSED_NB_WAVES 5
+#endif
+#ifndef RT_FUSED_NB
+#define RT_FUSED_NB 1
+#endif
+template <int ORDER, int PREC, bool LEVELS, bool GENPOW, bool NB>
+__global__ __launch_bounds__(256, NB ? RT_FUSED_NB_WAVES : RT_WAVES_PER_SIMD) void k_render(SceneHdr hdr, const double *__restrict__ tab,
                                                   const int *__restrict__ itab, int W, int H, int depth, int rb,
                                                   int shard, int nshards, int row0, int row_end, void *__restrict__ out,
                                                   uint8_t *__restrict__ levels, int levels_hit) {
@@ -1304,7 +1319,8 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
         for (int k = 0; k < depth; ++k) {
             double t = 0;
             int id = -1;
-            id = (k == 0) ? nearest<true>(S, 0, o, d, t, alive) : nearest<false>(S, 0, o, d, t, alive, prev);
+            id = (k == 0) ? nearest<true, false, 0, NB>(S, 0, o, d, t, alive)
+                           : nearest<false, false, 0, NB>(S, 0, o, d, t, alive, prev);
             if (id < 0) alive = false;
             prev = id;
             if (alive) {
@@ -1339,7 +1355,7 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
                 hit_geom(S, id, o2, d2, st[k * BLOCK + tid], hit, N);
             }
             const double refl = S.tab[hdr.o_obj + id * OBJ_W + 8];
-            const D3 F = shade<GENPOW>(S, id, d2, hit, N, col, refl, on);
+            const D3 F = shade<GENPOW, 0, NB>(S, id, d2, hit, N, col, refl, on);
             if (on) col = F;
         }
     } else {
@@ -1351,7 +1367,8 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
         for (int k = 0; k < depth; ++k) {
             double t = 0;
             int id = -1;
-            id = (k == 0) ? nearest<true>(S, 0, o, d, t, alive) : nearest<false>(S, 0, o, d, t, alive, prev);
+            id = (k == 0) ? nearest<true, false, 0, NB>(S, 0, o, d, t, alive)
+                           : nearest<false, false, 0, NB>(S, 0, o, d, t, alive, prev);
             if (id < 0) alive = false;
             prev = id;
             D3 hit = cam, N = cam;
@@ -1360,7 +1377,7 @@ __global__ RT_LAUNCH_BOUNDS void k_render(SceneHdr hdr, const double *__restrict
                 hit_geom(S, id, o, d, t, hit, N);
             }
             if (__all(!alive)) break;
-            const D3 F = shade<GENPOW>(S, alive ? id : 0, d, hit, N, D3{0.0, 0.0, 0.0}, 0.0, alive);
+            const D3 F = shade<GENPOW, 0, NB>(S, alive ? id : 0, d, hit, N, D3{0.0, 0.0, 0.0}, 0.0, alive);
             if (alive) {
                 col.x = col.x + w * F.x;
                 col.y = col.y + w * F.y;
@@ -1557,12 +1574,19 @@ int launch_t(rt_prepared *p, int W, int H, int depth, int rb, int shard, int nsh
     dim3 grid((W + TILE - 1) / TILE, (row_end - row0 + TILE - 1) / TILE);
     size_t lds = ORDER == RT_ORDER_EXACT ? (size_t)depth * BLOCK * 12 : 0;
     KtScope kt(p, RT_KT_RENDER, st);
-    if (levels)
-        hipLaunchKernelGGL((k_render<ORDER, PREC, true, GENPOW>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
-                           H, depth, rb, shard, nshards, row0, row_end, out, levels, levels_hit);
-    else
-        hipLaunchKernelGGL((k_render<ORDER, PREC, false, GENPOW>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab, p->d_itab, W,
-                           H, depth, rb, shard, nshards, row0, row_end, out, levels, levels_hit);
+    // scenes without wave beams (few spheres, e.g. the reference's own scene) take the beam-free build
+#define RT_K_RENDER(LV, NB)                                                                                            \
+    hipLaunchKernelGGL((k_render<ORDER, PREC, LV, GENPOW, NB>), grid, dim3(BLOCK), lds, st, p->hdr, p->d_tab,        \
+                       p->d_itab, W, H, depth, rb, shard, nshards, row0, row_end, out, levels, levels_hit)
+    const bool nb = RT_FUSED_NB && !p->hdr.beam_ok;
+    if (levels) {
+        if (nb) RT_K_RENDER(true, true);
+        else RT_K_RENDER(true, false);
+    } else {
+        if (nb) RT_K_RENDER(false, true);
+        else RT_K_RENDER(false, false);
+    }
+#undef RT_K_RENDER
     HIPCHK(hipGetLastError());
     return RT_OK;
 }
