@@ -105,6 +105,20 @@ __device__ __forceinline__ double div_n(double a, double b) {
     return __builtin_fma(r, y, q);
 }
 
+// a / n for a frame dimension n (W, H; 1 <= n <= 2^20) and 0 <= a < 2^44 exactly representable:
+// for a power of two the quotient is exact, so the correctly rounded division is the exponent
+// shift (one v_ldexp_f64 instead of v_rcp_f64 and seven fma / mul) — the same bits
+__device__ __forceinline__ double div_dim(double a, int n) {
+    if ((n & (n - 1)) == 0) return __builtin_amdgcn_ldexp(a, -__builtin_ctz((unsigned)n)); // (wave-uniform)
+    return div_n(a, (double)n);
+}
+// floor(a / n) for 0 <= a < 2^31, 1 <= n <= 2^20: a shift for a power of two; otherwise the
+// correctly rounded binary64 quotient, which truncates to the exact integer quotient
+__device__ __forceinline__ int idiv_dim(int a, int n) {
+    if ((n & (n - 1)) == 0) return a >> __builtin_ctz((unsigned)n); // (wave-uniform)
+    return (int)div_n((double)a, (double)n);
+}
+
 // FAST: the caller guarantees x is in range (a sphere test's discriminant, >= 0.001 or 1.0 by
 // then, in a spheres-only scene within CULL_EXTENT: every ray is a unit vector — primary rays and
 // shadow rays are normalised, reflections off spheres keep the length — so disc <= ~1e10, far

@@ -9,6 +9,7 @@ export PYTHONUNBUFFERED=1
 lib() { if [ "$1" = cur ]; then echo ""; else echo "RT_LIB_PATH=eraytracer_amd/variants/librtmi355x_$1.so"; fi; }
 for v in "$@"; do
   [ "$v" = cur ] && continue
+  [ "${PARITY_K:-brute}" = none ] && continue
   timeout -k 10 300 env $(lib $v) python -u -m pytest ${PARITY_FILES:-tests/test_gpu_frames.py} -k "${PARITY_K:-brute}" -q \
       --timeout 250 --timeout-method thread > gpurun_out/abn_parity_$v.log 2>&1 || { echo "PARITY FAIL $v"; tail -5 gpurun_out/abn_parity_$v.log; exit 1; }
   echo "parity ok $v"
