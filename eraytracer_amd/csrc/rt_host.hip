@@ -396,6 +396,47 @@ int rt_host_free(void *p) {
     return RT_OK;
 }
 
+// Device memory held by the idle contexts of `device` (their work space and output buffers), freed
+// so that a caller whose allocation failed can retry: the pool caps contexts by count, and each
+// keeps what its largest frame needed (about 5 GB at 4096^2 depth 5), so idle ones can crowd out
+// a busy one.  Returns the bytes freed (0: nothing to free, the failure stands).
+static size_t trim_idle(int device) {
+    std::vector<rt_ctx *> idle;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (rt_ctx *c : pool())
+            if (c->device == device && !c->busy) {
+                c->busy = true; // claimed while trimmed
+                idle.push_back(c);
+            }
+    }
+    size_t freed = 0;
+    for (rt_ctx *c : idle) {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->render);
+        (void)hipStreamSynchronize(c->copy);
+        (void)hipStreamSynchronize(c->copy2);
+        if (c->p) freed += rt_trim(c->p);
+        for (int i = 0; i < 3; ++i) {
+            if (c->d_buf[i]) (void)hipFree(c->d_buf[i]);
+            freed += c->d_cap[i];
+            c->d_buf[i] = nullptr;
+            c->d_cap[i] = 0;
+        }
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    if (!idle.empty()) {
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            for (rt_ctx *c : idle) c->busy = false;
+        }
+        g_cv.notify_all();
+    }
+    return freed;
+}
+
 int rt_reset_contexts(void) {
     std::vector<rt_ctx *> dead;
     int busy = 0;
@@ -484,9 +525,16 @@ int rt_render(const rt_elem *scene, uint32_t n, uint32_t width, uint32_t height,
         rt_ctx *c = ctx[d];
         (void)hipSetDevice(dev);
         const uint32_t k = shards_of(d);
+        // an allocation that fails while other contexts of the device sit idle on their memory is
+        // retried once after those are trimmed (trim_idle)
         err = rt_ctx_device_buffer(c, 0, k * slab_bytes, reinterpret_cast<void **>(&d_out[d]));
-        if (err == RT_OK && o.out_levels)
+        if (err == RT_ENOMEM && trim_idle(dev) > 0)
+            err = rt_ctx_device_buffer(c, 0, k * slab_bytes, reinterpret_cast<void **>(&d_out[d]));
+        if (err == RT_OK && o.out_levels) {
             err = rt_ctx_device_buffer(c, 1, (size_t)k * slab * width, reinterpret_cast<void **>(&d_lv[d]));
+            if (err == RT_ENOMEM && trim_idle(dev) > 0)
+                err = rt_ctx_device_buffer(c, 1, (size_t)k * slab * width, reinterpret_cast<void **>(&d_lv[d]));
+        }
         if (err == RT_OK && !pinned) err = rt_ctx_host_buffer(c, 2 * (size_t)band * rowbytes, reinterpret_cast<void **>(&stage[d]));
         if (err != RT_OK) break;
         if (hipEventRecord(c->e0, c->render) != hipSuccess) err = RT_EHIP;
@@ -499,6 +547,9 @@ int rt_render(const rt_elem *scene, uint32_t n, uint32_t width, uint32_t height,
                 const uint32_t b0 = b * band, b1 = std::min(slab, b0 + band);
                 err = rt_launch_rows(c->p, width, height, depth, rb, s, ns, o.precision, o.order, o.spp, o.seed, b0,
                                      b1, slab_out, slab_lv, c->render, (o.flags & RT_LEVELS_HIT) ? 1 : 0);
+                if (err == RT_ENOMEM && trim_idle(dev) > 0) // (a failed grow launches nothing)
+                    err = rt_launch_rows(c->p, width, height, depth, rb, s, ns, o.precision, o.order, o.spp, o.seed,
+                                         b0, b1, slab_out, slab_lv, c->render, (o.flags & RT_LEVELS_HIT) ? 1 : 0);
                 if (err == RT_OK && hipEventRecord(c->band[i * nb + b], c->render) != hipSuccess) err = RT_EHIP;
                 if (err == RT_OK && pinned) {
                     hipStream_t cs = ((i * nb + b) % copy_streams()) ? c->copy2 : c->copy;

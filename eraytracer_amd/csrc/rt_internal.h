@@ -20,6 +20,11 @@ int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dep
 // kept; captured frame graphs are invalidated).  No launch of p may be in flight.
 int rt_prepare_scene(rt_prepared *p, const rt_elem *scene, uint32_t n);
 
+// Free p's wavefront work space (queues, colours, flags, lists, supersampling sums, primary
+// masks: GBs at 4096^2); the next launch grows it again.  No launch of p may be in flight.
+// Returns the bytes freed.
+size_t rt_trim(rt_prepared *p);
+
 // ---- the process's render contexts (rt_host.hip) ------------------------------------------
 // One context = one device, two streams (render, copy), the most recently prepared scene with
 // its grown work space, grown device output buffers and a pinned host staging buffer.  The

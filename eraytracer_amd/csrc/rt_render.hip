@@ -1821,6 +1821,30 @@ int rt_release(rt_prepared *p) {
 
 } // extern "C"
 
+// Free the wavefront work space of an idle context (rt_internal.h); the next launch regrows it.
+size_t rt_trim(rt_prepared *p) {
+    if (!p) return 0;
+    DevGuard g(p->device);
+    size_t freed = 0;
+    auto drop = [&](void *&b, size_t &n) {
+        if (b) (void)hipFree(b);
+        b = nullptr;
+        freed += n;
+        n = 0;
+    };
+    drop(p->d_queue, p->queue_bytes);
+    drop(reinterpret_cast<void *&>(p->d_colbuf), p->colbuf_bytes);
+    drop(reinterpret_cast<void *&>(p->d_child), p->child_bytes);
+    drop(reinterpret_cast<void *&>(p->d_lit), p->lit_bytes);
+    drop(reinterpret_cast<void *&>(p->d_sample), p->sample_bytes);
+    drop(reinterpret_cast<void *&>(p->d_counts), p->counts_bytes);
+    drop(reinterpret_cast<void *&>(p->d_items), p->items_bytes);
+    drop(reinterpret_cast<void *&>(p->d_pmask), p->pmask_bytes);
+    p->pmask_valid = false;
+    ++p->gen; // captured frame graphs hold the old pointers
+    return freed;
+}
+
 namespace {
 
 // Queue memory per pass is bounded (RT_QUEUE_MB, default 8 GiB); taller slabs are rendered
