@@ -173,7 +173,12 @@ int rt_scene_canon(rt_elem *scene, uint32_t n_elems);
  * rendered in row bands whose copies to the host overlap the next band's render; memory from
  * rt_host_alloc (or registered with HIP) is written by DMA directly, other memory through a
  * pinned staging ring.  Thread-safe: concurrent callers get separate contexts (up to 4 per
- * device; more wait). */
+ * device; more wait).  Device memory per context: the wavefront work space of the largest frame
+ * it rendered (~5 GB at 4096^2 depth 5: 64-byte hit records per level and 16x16-tile slot,
+ * colours, flags, lists; spp > 1 adds the binary64 sums, 24 B per pixel) plus its output
+ * buffers (the frame, 201 MB at 4096^2 f32); it is kept while the context is idle.  An
+ * allocation that fails while other contexts of the device are idle is retried once after their
+ * memory is freed (a busy context's is never touched); rt_reset_contexts frees it all. */
 int rt_render(const rt_elem *scene, uint32_t n_elems, uint32_t width, uint32_t height,
               uint32_t depth, const rt_opts *opts, void *out_rgb, rt_stats *stats);
 
