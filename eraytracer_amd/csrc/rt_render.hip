@@ -255,6 +255,24 @@ struct Scene {
     const int *__restrict__ itab;
 };
 
+// The scene header re-read from the kernel argument segment (scalar loads; every kernel here takes
+// the SceneHdr its Scene holds as its first argument) instead of being held in SGPRs across a
+// long loop: the kernels' uniform values exceed the SGPR file, and spilled ones come back through
+// v_readlane on every use (measured on k_reflect_shade: SGPR spills 90 -> 21, config 3 +2 %).
+#ifndef RT_HDR_RELOAD
+#define RT_HDR_RELOAD 1
+#endif
+__device__ __forceinline__ Scene fresh_scene(const Scene &S) {
+#if RT_HDR_RELOAD && defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(4))) const SceneHdr KHdr;
+    KHdr *hp = (KHdr *)(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(hp)); // opaque: the loads stay where the values are used
+    return Scene{*hp, S.tab, S.itab};
+#else
+    return S;
+#endif
+}
+
 // ---- scene table access; SPH (template argument of the shading code): 0 = any scene, 1 = spheres
 // only (occluder masks), 2 = spheres only with the per-lane-gathered tables staged in LDS.
 // Lanes of a wave read these rows by their own object / target / candidate (gathers whose L2
@@ -1255,13 +1273,14 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
     RT_STAT(ST_SHADE, 1);
     D3 F = {0.0, 0.0, 0.0};
     for (int i = 0; i < h.n_light; ++i) {
-        const double *L = S.tab + h.o_light + i * LIGHT_W;
+        const Scene &SL = S; // (re-reading the header per light, fresh_scene: measured neutral)
+        const double *L = SL.tab + SL.h.o_light + i * LIGHT_W;
         const D3 Lc = {L[0], L[1], L[2]}, Lp = {L[3], L[4], L[5]}, Sc = {L[6], L[7], L[8]};
         const double2 m34 = *reinterpret_cast<const double2 *>(m + 4), m67 = *reinterpret_cast<const double2 *>(m + 6);
         const D3 mc = {m[3], m34.x, m34.y};
         const double spow = m67.x, shin = m67.y;
         // diffuse_term/4 (:272-279)
-        const D3 ln = normalize3(D3{Lp.x - hit.x, Lp.y - hit.y, Lp.z - hit.z}, SPH && h.norm_ok);
+        const D3 ln = normalize3(D3{Lp.x - hit.x, Lp.y - hit.y, Lp.z - hit.z}, SPH && SL.h.norm_ok);
         const double dd = max0(dot3(N, ln));
         const D3 diff = {mc.x * dd, mc.y * dd, mc.z * dd};
         // specular_term/7 (:285-297)
@@ -1274,7 +1293,7 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
         const D3 lc = {Lc.x * con.x, Lc.y * con.y, Lc.z * con.z};
         const bool need = active && !(lc.x == 0.0 && lc.y == 0.0 && lc.z == 0.0);
         // shadow ray direction normalize(Hit - Light) == -normalize(Light - Hit), bit for bit
-        const bool lb = lit_by<SPH, NB>(S, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp);
+        const bool lb = lit_by<SPH, NB>(SL, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp);
         if (bits && lb && i < 32) *bits |= 1u << i;
         const double lit = lb ? 1.0 : 0.0;
         F.x = F.x + (col.x * refl + lc.x * lit);
