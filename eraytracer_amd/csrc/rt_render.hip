@@ -1350,10 +1350,11 @@ __global__ __launch_bounds__(256, NB ? RT_FUSED_NB_WAVES : RT_WAVES_PER_SIMD) vo
         bool alive = active;
         int prev = -1;
         for (int k = 0; k < depth; ++k) {
+            const Scene SL = fresh_scene(S); // the header re-read per level (fresh_scene)
             double t = 0;
             int id = -1;
-            id = (k == 0) ? nearest<true, false, 0, NB>(S, 0, o, d, t, alive)
-                           : nearest<false, false, 0, NB>(S, 0, o, d, t, alive, prev);
+            id = (k == 0) ? nearest<true, false, 0, NB>(SL, 0, o, d, t, alive)
+                           : nearest<false, false, 0, NB>(SL, 0, o, d, t, alive, prev);
             if (id < 0) alive = false;
             prev = id;
             if (alive) {
@@ -1364,7 +1365,7 @@ __global__ __launch_bounds__(256, NB ? RT_FUSED_NB_WAVES : RT_WAVES_PER_SIMD) vo
             }
             if (alive) {
                 D3 hit, N;
-                hit_geom(S, id, o, d, t, hit, N);
+                hit_geom(SL, id, o, d, t, hit, N);
                 d = bounce3(d, N);
                 o = hit;
             }
@@ -1374,21 +1375,22 @@ __global__ __launch_bounds__(256, NB ? RT_FUSED_NB_WAVES : RT_WAVES_PER_SIMD) vo
         int maxlev = 0;
         while (maxlev < depth && __ballot(nlev > maxlev) != 0) ++maxlev; // wave-wide max level
         for (int m = 0; m < maxlev; ++m) {
+            const Scene SL = fresh_scene(S); // the header re-read per level (fresh_scene)
             const int k = nlev - 1 - m;
             const bool on = k >= 0;
             D3 o2 = cam, d2 = d0, hit = cam, N = cam;
             int id = 0;
             if (on) {
                 for (int j = 0; j < k; ++j) { // replay the chain to level k
-                    hit_geom(S, so[j * BLOCK + tid], o2, d2, st[j * BLOCK + tid], hit, N);
+                    hit_geom(SL, so[j * BLOCK + tid], o2, d2, st[j * BLOCK + tid], hit, N);
                     d2 = bounce3(d2, N);
                     o2 = hit;
                 }
                 id = so[k * BLOCK + tid];
-                hit_geom(S, id, o2, d2, st[k * BLOCK + tid], hit, N);
+                hit_geom(SL, id, o2, d2, st[k * BLOCK + tid], hit, N);
             }
-            const double refl = S.tab[hdr.o_obj + id * OBJ_W + 8];
-            const D3 F = shade<GENPOW, 0, NB>(S, id, d2, hit, N, col, refl, on);
+            const double refl = SL.tab[SL.h.o_obj + id * OBJ_W + 8];
+            const D3 F = shade<GENPOW, 0, NB>(SL, id, d2, hit, N, col, refl, on);
             if (on) col = F;
         }
     } else {
