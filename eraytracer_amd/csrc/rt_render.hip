@@ -1512,8 +1512,12 @@ struct rt_prepared {
     hipEvent_t ev_lit[RT_MAX_DEPTH + 1] = {};   // level k is shaded
     // Frames repeat with identical arguments (bench, multi-GPU renderer): the second identical
     // rt_launch captures the frame's launch sequence into a graph, later ones replay it.
-    // gen counts work-space reallocations, which invalidate captured pointers.
+    // gen counts changes that invalidate a captured frame: work-space reallocations (captured
+    // pointers), new scene tables or header, and recomputed primary candidate masks (a graph
+    // captured while they were valid holds no k_pmask launch).
     unsigned gen = 0;
+    // scene_gen counts new scene tables and culling changes (the primary masks depend on them)
+    unsigned scene_gen = 0;
     // RT_CFG_KERNEL_TIMING: per timed kernel (RT_KT_* bit i), a ring of event pairs; a full ring
     // folds its oldest pair into the sum (waiting for it)
     int timing_mask = 0;
@@ -1762,6 +1766,7 @@ int rt_prepare_scene(rt_prepared *p, const rt_elem *scene, uint32_t n) {
     p->hdr_full = c.hdr;
     apply_cull(p);
     ++p->gen; // captured graphs hold the old tables
+    ++p->scene_gen;
     p->last_valid = false;
     return RT_OK;
 }
@@ -1784,6 +1789,7 @@ int rt_configure(rt_prepared *p, int option, int64_t value) {
         p->cull = (int)value;
         apply_cull(p);
         ++p->gen; // captured graphs hold the old header
+        ++p->scene_gen;
         p->last_valid = false;
         return RT_OK;
     default:
@@ -1981,16 +1987,18 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     if (rc == RT_OK && overlap) rc = side_stream(p);
     if (rc != RT_OK) return rc;
     // the primary rays' candidate masks of the whole slab (k_pmask), recomputed only when the
-    // frame geometry, the scene or the work space (gen) changed
+    // frame geometry or the scene changed (or after rt_trim)
     const unsigned long long *pmask = nullptr;
     if (p->hdr.beam_ok && D > 0 && pmask_on()) {
         const int slab_all = (int)rt_shard_rows(H, rb, ns);
         const size_t nhalf = (size_t)tiles_x * ((slab_all + TILE - 1) / TILE) * 2;
-        const long long key[8] = {W, H, rb, sh, ns, spp > 1, (long long)p->gen, slab_all};
+        const long long key[8] = {W, H, rb, sh, ns, spp > 1, (long long)p->scene_gen, slab_all};
         if (!(p->pmask_valid && std::memcmp(key, p->pmask_key, sizeof(key)) == 0)) {
             p->pmask_valid = false;
-            unsigned dummy = 0; // (not part of the captured work space: gen untouched)
-            if ((rc = grow(reinterpret_cast<void **>(&p->d_pmask), &p->pmask_bytes, nhalf * p->hdr.n_chunk * 8, &dummy)) !=
+            // New masks (and perhaps a new buffer): a frame graph captured with the old ones holds
+            // no k_pmask launch and would read these, so it is invalidated (gen).
+            ++p->gen;
+            if ((rc = grow(reinterpret_cast<void **>(&p->d_pmask), &p->pmask_bytes, nhalf * p->hdr.n_chunk * 8, &p->gen)) !=
                 RT_OK)
                 return rc;
             const dim3 pg((unsigned)std::min<size_t>(4096, (nhalf + 3) / 4));
@@ -2248,7 +2256,14 @@ int launch_frame(rt_prepared *p, const long long (&args)[12], hipStream_t st, F 
     const int rc = enqueue(p->cap);
     hipGraph_t gr = nullptr;
     const hipError_t e = hipStreamEndCapture(p->cap, &gr);
-    if (rc != RT_OK || e != hipSuccess || (long long)p->gen != key[11]) {
+    if (rc == RT_OK && e == hipSuccess && (long long)p->gen != key[11]) {
+        // the work space or the primary masks changed while capturing: nothing was run — drop
+        // the graph and render this frame directly
+        (void)hipGraphDestroy(gr);
+        p->last_valid = false;
+        return enqueue(st);
+    }
+    if (rc != RT_OK || e != hipSuccess) {
         if (gr) (void)hipGraphDestroy(gr);
         p->last_valid = false;
         return rc != RT_OK ? rc : RT_EHIP;
@@ -2287,8 +2302,9 @@ bool use_mega_engine(const rt_prepared *p) {
     if (mode) return mode == 1;
     // spheres-only scenes whose tables are staged in LDS: the wavefront engine at every size
     // (measured round 2, 4096^2 d5, 4 frames in flight: S4 115 vs 89 Gpx/s, S8 86 vs 70,
-    // S16 58 vs 42, S24 49 vs 37, S32 52 vs 38)
-    const SceneHdr &h = p->hdr;
+    // S16 58 vs 42, S24 49 vs 37, S32 52 vs 38).  Decided from the compiled header, not the one
+    // RT_CFG_CULL = 0 strips, so the brute-force mode runs the production engine.
+    const SceneHdr &h = p->hdr_full;
     if (h.n_tri == 0 && h.n_pl == 0 && h.cull_ok && h.l_bytes > 0) return false;
     return h.n_obj <= max_obj;
 }
@@ -2363,8 +2379,8 @@ int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dep
             if (wave_single_write(p, D, lv != nullptr && !levels_hit)) {
                 // every pixel written once: the pass folds its sample into acc (and the last one
                 // writes the output) itself — no sample slab, no k_accum
-#define RT_SS(P) (p->hdr.int_pow ? launch_wavefront<P, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, lv, st, (int)spp, s, seed, acc, 1) \
-                                 : launch_wavefront<P, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, lv, st, (int)spp, s, seed, acc, 1))
+#define RT_SS(P) (p->hdr.int_pow ? launch_wavefront<P, false>(p, W, H, D, rb, sh, ns, r0, r1, d_out, lv, st, (int)spp, s, seed, acc, levels_hit) \
+                                 : launch_wavefront<P, true>(p, W, H, D, rb, sh, ns, r0, r1, d_out, lv, st, (int)spp, s, seed, acc, levels_hit))
                 rc = precision == RT_OUT_F64 ? RT_SS(RT_OUT_F64) : RT_SS(RT_OUT_F32);
 #undef RT_SS
                 if (rc != RT_OK) return rc;

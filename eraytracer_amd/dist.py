@@ -249,8 +249,10 @@ class CompactGather:
         self.headed.append((b, cev))
 
     def _send(self, b, cev):
-        """Frame in slot b: read its counts on the host (waiting for their copy alone), then
-        send the values to rank 0."""
+        """Frame in slot b: read its counts on the host, then send the values to rank 0.  The
+        host waits for the counts' copy event, which the side stream orders after its earlier
+        work as well (older frames' decode and transfer waits): by then, with frames in flight,
+        those are normally done."""
         import torch.distributed as dist
         with self._side():
             if cev is not None:

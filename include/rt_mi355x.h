@@ -132,7 +132,11 @@ typedef struct rt_opts {
  *     X = (x + u) / W,  Y = (y + v) / H                                 (binary64)
  * and the pixel is (c_0 + c_1 + ... + c_{spp-1}) / spp, summed left to right in binary64.
  * spp = 1 is the reference's X = x/W, Y = y/H exactly.  out_levels / d_levels report
- * sample 0. */
+ * sample 0 (its chain's level count, or with RT_LEVELS_HIT its primary-hit mask).
+ * Levels count the objects a pixel's reflection chain hit (0 = background).  A scene without
+ * point lights traces no reflections (the reference's fold over the lights never recurses,
+ * raytracer.erl:209-252), so there a pixel's level is at most 1 with or without RT_LEVELS_HIT;
+ * so it is at depth 1. */
 #define RT_MAX_SPP 4096
 
 typedef struct rt_stats {

@@ -121,7 +121,10 @@ def load_trace(d, timed=None, iso=0):
     frame = {"frames": len(fr), "kernels_per_frame": len(fr[0]), "avg_busy_ns": sum(busy) / len(busy),
              "avg_span_ns": sum(span) / len(span), "min_busy_ns": min(busy),
              "window_ns_per_frame": (t_last - t_first) / len(tf), "window_frames": len(tf)}
-    kern = {lab: {"avg_ns": sum(v) / len(v), "vgpr": vg[lab]} for lab, v in per.items()}
+    # rocprofv3's VGPR_Count on gfx950 is half the allocated VGPRs (48 for the compiler's 96-VGPR
+    # kernels: checked against -Rpass-analysis=kernel-resource-usage, profiles/*_resource_usage.txt)
+    kern = {lab: {"avg_ns": sum(v) / len(v), "rocprof_vgpr_count": vg[lab], "vgpr_alloc": 2 * vg[lab]}
+            for lab, v in per.items()}
     for lab, v in iso_k.items():
         kern.setdefault(lab, {})["isolated_avg_ns"] = sum(v) / len(v)
     return frame, kern
@@ -182,7 +185,7 @@ def main():
     for lab, e in out["kernels"].items():
         x = e["derived"]
         print(f"{lab:14s} {e.get('avg_ns', 0) / 1e3:8.1f} us (alone {e.get('isolated_avg_ns', 0) / 1e3:6.1f}) "
-              f"vgpr={e.get('vgpr')} "
+              f"vgpr_alloc={e.get('vgpr_alloc', 2 * e.get('vgpr', 0))} "
               f"valu/wave={x.get('valu_insts_per_wave', 0):8.0f} f64frac={x.get('f64_issue_frac_of_peak_39.3T', 0):.3f} "
               f"valu_share={x.get('sq_active_inst_valu_share', 0):.3f} lanes={x.get('valu_lane_utilisation', 0):.2f}")
 

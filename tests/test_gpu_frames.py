@@ -142,8 +142,9 @@ def test_s256_d8_every_pixel_bench_path(oracle):
     ("s64", 4096, 4096, 5, 1, 1.5),       # config 3
     ("s256", 4096, 4096, 8, 1, 2.0),      # config 5's scene and depth, one sample
     ("s256", 4096, 4096, 8, 16, 2.0),     # config 5 itself
-    ("s16", 2048, 2048, 5, 1, 0),         # LDS-staged spheres, below the BVH and cell thresholds (brute
-                                          # force picks the fused engine there: no time comparison)
+    ("s64", 8192, 8192, 5, 1, 1.5),       # config 4's frame geometry (its own primary candidate masks)
+    ("s16", 2048, 2048, 5, 1, 1.1),       # LDS-staged spheres, below the BVH and cell thresholds (the
+                                          # brute force runs the same wavefront engine, unstaged)
     ("mixed", 1536, 1024, 5, 1, 1.15),    # spheres + triangles + planes: shadow cones, scanned types
     ("default", 1920, 1080, 5, 1, 0),     # config 2 (fused engine; 3 spheres: below the beams' minimum)
 ])

@@ -86,8 +86,9 @@ def test_config3_s64_4096_d5_256_rows(oracle):
 
 def test_config4_s64_8192_d5_shards(oracle):
     """BASELINE config 4 (S64, 8192x8192, depth 5, rows over 8 GPUs): the 8-way interleaved row
-    split through rt_render (8 shards on this device) equals the 1-shard frame bit for bit,
-    and 32 sampled rows equal the oracle."""
+    split through rt_render (8 shards on this device) equals the 1-shard frame bit for bit, and
+    512 rows (64 bands of 8 rows spread over the frame: 4.2 M pixels, 6 % of it) equal the oracle
+    — identical levels, max |delta| <= 1e-5 on the binary32 frame."""
     scene = scenes.s64()
     W = H = 8192
     one, lv = render(W, H, scene, 5, precision="f32", levels=True)
@@ -96,10 +97,12 @@ def test_config4_s64_8192_d5_shards(oracle):
     assert np.array_equal(one.view(np.int32), eight.view(np.int32))
     del eight
     el = N.marshal(scene)
-    for r in _rows(H, 32):
-        ref, rlv = oracle.render(el, W, H, 5, mode=oracle.MEMO, row0=r, nrows=1, levels=True)
-        np.testing.assert_array_equal(lv[r:r + 1], rlv)
-        assert np.abs(one[r:r + 1].astype(np.float64) - ref).max() <= TOL, r
+    bands = _rows(H - 8, 64)
+    for i, r in enumerate(bands):
+        ref, rlv = oracle.render(el, W, H, 5, mode=oracle.MEMO, row0=r, nrows=8, levels=True)
+        _compare(one[r:r + 8], lv[r:r + 8], ref, rlv, f"config 4 rows {r}-{r + 7}", 0)
+        if i % 16 == 15:
+            print(f"  config 4: {i + 1} of {len(bands)} bands checked", flush=True)
 
 
 def test_config5_s256_4096_d8_spp16_rows(oracle):

@@ -196,6 +196,50 @@ def test_repeated_launch_graph_replay(oracle):
         L.rt_release(p)
 
 
+def test_frame_graphs_follow_the_primary_masks():
+    """Frame graphs on (RT_GRAPH=1, read once per process: a child).  One context alternates two
+    shards of a frame and a second frame geometry, so the primary rays' candidate masks (k_pmask,
+    recomputed when the geometry or shard changes) are rewritten between identical launches that
+    would otherwise replay a captured graph holding no k_pmask launch: every launch must equal the
+    same frame from a fresh context (graphs off there: first launches run directly), bit for bit."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r"""
+import ctypes, numpy as np, torch
+from eraytracer_amd import _native as N, scenes
+L = N.lib()
+el = N.marshal(scenes.s64())
+st = torch.cuda.current_stream().cuda_stream
+def launch(p, w, h, shard, ns):
+    rows = L.rt_shard_rows(h, 16, ns)
+    out = torch.full((rows, w, 3), float('nan'), dtype=torch.float64, device='cuda')
+    N.check(L.rt_launch(p, w, h, 5, 16, shard, ns, N.RT_OUT_F64, N.RT_ORDER_EXACT, out.data_ptr(), None, st))
+    torch.cuda.synchronize()
+    return np.nan_to_num(out.cpu().numpy(), nan=-7.0)
+def fresh(w, h, shard, ns):
+    q = ctypes.c_void_p()
+    N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(q)))
+    try:
+        N.check(L.rt_configure(q, N.RT_CFG_SIDE_STREAMS, 0))
+        return launch(q, w, h, shard, ns)
+    finally:
+        L.rt_release(q)
+p = ctypes.c_void_p()
+N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(p)))
+N.check(L.rt_configure(p, N.RT_CFG_SIDE_STREAMS, 0))
+seq = [(256, 192, 0, 2)] * 3 + [(256, 192, 1, 2)] * 3 + [(256, 192, 0, 2)] * 3 + [(160, 96, 0, 1)] * 3 + \
+      [(256, 192, 1, 2), (256, 192, 0, 2), (256, 192, 0, 2), (256, 192, 0, 2)]
+ref = {a: fresh(*a) for a in set(seq)}
+for i, a in enumerate(seq):
+    got = launch(p, *a)
+    assert np.array_equal(got.view(np.int64), ref[a].view(np.int64)), (i, a)
+L.rt_release(p)
+print('ok')
+"""
+    env = dict(os.environ, RT_GRAPH="1", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout.split(), r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("name,w,h,d,spp", [("s64", 48, 40, 5, 4), ("default", 40, 32, 5, 3), ("s256", 32, 24, 8, 16)])
 def test_supersampling_matches_oracle(oracle, name, w, h, d, spp):
     """BASELINE config 5's stochastic supersampling (RT_SUPERSAMPLING) against the oracle's
