@@ -2127,7 +2127,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
 #define RT_RS(SPHV, ILPV, LDSV, BVHV)                                                                               \
     hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV>), dim3(sblocks), dim3(BLOCK), LDSV, st, rhdr,   \
                        p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
-                       colk(k - 1), litk(k - 1), g)
+                       colk(k - 1), g)
                 // levels traversing the sphere BVH (unstaged scenes only): the BVH instantiations
                 const bool bvh_k = !staged && rhdr.bvh_ok && k >= rhdr.bvh_level;
                 if (staged && k == 1) RT_RS(2, false, lds, false);
@@ -2162,18 +2162,21 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         if (nrefl > 0) {
             const size_t ls_ = (size_t)ntiles * TILE_SLOTS;
             const bool bits = p->hdr.n_light <= 32; // the shadow answers fit the record
-            // deep: the merged walk (no k_walk_deep; without side streams)
+            // deep: the merged walk (no k_walk_deep; without side streams); after k_reflect_shade
+            // (fuse) the shadow answers are in the children's records (PAD)
             auto walk = [&](hipStream_t s_, int lo, int hi, bool deep) {
+#define RT_WALK_K(SPHV, BITSV, DEEPV, PADV, LDSV)                                                                    \
+    hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV, DEEPV, PADV>), dim3(sblocks), dim3(BLOCK), LDSV, s_,       \
+                       p->hdr, p->d_tab, p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child,  \
+                       p->d_lit, lo, hi, g)
 #define RT_WALK(SPHV, BITSV, LDSV)                                                                                  \
     do {                                                                                                           \
-        if (deep)                                                                                                  \
-            hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV, true>), dim3(sblocks), dim3(BLOCK), LDSV, s_,     \
-                               p->hdr, p->d_tab, p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf,      \
-                               p->d_child, p->d_lit, lo, hi, g);                                                    \
+        if (deep && fuse && BITSV)                                                                                 \
+            RT_WALK_K(SPHV, BITSV, true, true, LDSV);                                                              \
+        else if (deep)                                                                                             \
+            RT_WALK_K(SPHV, BITSV, true, false, LDSV);                                                             \
         else                                                                                                       \
-            hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV, false>), dim3(sblocks), dim3(BLOCK), LDSV, s_,    \
-                               p->hdr, p->d_tab, p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf,      \
-                               p->d_child, p->d_lit, lo, hi, g);                                                    \
+            RT_WALK_K(SPHV, BITSV, false, false, LDSV);                                                            \
     } while (0)
                 if (staged && bits) RT_WALK(2, true, lds);
                 else if (staged) RT_WALK(2, false, lds);
@@ -2182,6 +2185,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                 else if (bits) RT_WALK(0, true, 0);
                 else RT_WALK(0, false, 0);
 #undef RT_WALK
+#undef RT_WALK_K
             };
             if (overlap) { // side stream 0 (after level 0's shading) waits for level 1's, and for
                            // k_reflect(2), which marks the level-1 records that have a child

@@ -18,10 +18,10 @@ USED = {
     "k_items": "c3 c4 c5",
     "k_reflect_shade<1,false,2,false,false>": "c3 c4 (level 1)",
     "k_reflect_shade<1,false,2,true,false>": "c3 c4 (levels 2-4)",
-    "k_walk<1,false,2,true,true>": "c3 c4",
+    "k_walk<1,false,2,true,true,true>": "c3 c4",
     "k_reflect_shade<1,false,1,false,false>": "c5 (level 1)",
     "k_reflect_shade<1,false,1,true,true>": "c5 (levels 2-7, BVH)",
-    "k_walk<1,false,1,true,true>": "c5",
+    "k_walk<1,false,1,true,true,true>": "c5",
 }
 
 
