@@ -6,6 +6,9 @@ identical (checked exactly through the per-pixel level counts) and colours diffe
 where device pow() rounds differently from the host libm (~1e-16).
 """
 import ctypes
+import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
