@@ -1493,8 +1493,10 @@ struct rt_prepared {
     size_t colbuf_bytes = 0;
     int *d_counts = nullptr;  // per level and tile: queue lengths
     size_t counts_bytes = 0;
-    int *d_items = nullptr;   // per-level record counts, then per-level dense slot lists
+    int *d_items = nullptr;   // per-level record counts and sort histograms, then per-level dense slot lists
     size_t items_bytes = 0;
+    int2 *d_keyrank = nullptr; // sorted levels: per level and slot, the record's (bin, rank in the bin)
+    size_t keyrank_bytes = 0;
     // primary rays' candidate masks per 8x16 pixel block of the slab (k_pmask), kept while the
     // frame geometry and the scene stay the same
     unsigned long long *d_pmask = nullptr;
@@ -1829,6 +1831,7 @@ int rt_release(rt_prepared *p) {
     if (p->d_sample) (void)hipFree(p->d_sample);
     if (p->d_counts) (void)hipFree(p->d_counts);
     if (p->d_items) (void)hipFree(p->d_items);
+    if (p->d_keyrank) (void)hipFree(p->d_keyrank);
     if (p->d_pmask) (void)hipFree(p->d_pmask);
     for (hipEvent_t &e : p->ev_level)
         if (e) (void)hipEventDestroy(e);
@@ -1866,6 +1869,7 @@ size_t rt_trim(rt_prepared *p) {
     drop(reinterpret_cast<void *&>(p->d_sample), p->sample_bytes);
     drop(reinterpret_cast<void *&>(p->d_counts), p->counts_bytes);
     drop(reinterpret_cast<void *&>(p->d_items), p->items_bytes);
+    drop(reinterpret_cast<void *&>(p->d_keyrank), p->keyrank_bytes);
     drop(reinterpret_cast<void *&>(p->d_pmask), p->pmask_bytes);
     p->pmask_valid = false;
     ++p->gen; // captured frame graphs hold the old pointers
@@ -1939,6 +1943,16 @@ bool fuse_on() {
     return on;
 }
 
+// Sorted deep levels (SORT_BINS): RT_SORT=0 off, 1 (default) scenes with the sphere BVH (many
+// spheres: incoherent deep levels), 2 every spheres-only scene — for A/B runs.
+int sort_mode() {
+    static const int m = [] {
+        const char *e = std::getenv("RT_SORT");
+        return e ? std::atoi(e) : 1;
+    }();
+    return m;
+}
+
 // Does a wavefront pass write every pixel exactly once?  Yes with k_reflect_shade (the colours of
 // records with a reflection hit are left to k_walk) and without reflections; no when k_light
 // shades level 0 provisionally beside the chain (side streams, or levels requested).
@@ -1979,11 +1993,19 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         rc = grow(reinterpret_cast<void **>(&p->d_lit), &p->lit_bytes, slots * nlev * sizeof(unsigned), &p->gen);
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_counts), &p->counts_bytes, max_tiles * nlev * sizeof(int), &p->gen);
-    // dense work lists: 64 per-level record counts, then per level the slots of its records
-    const size_t items_ints = slots * nlev + 64;
+    const bool overlap = lit_overlap(p) && D > 1 && p->hdr.n_light > 0;
+    // levels 1 .. nrefl - 1 (each shaded and reflected by k_reflect_shade) listed in sort-key order
+    const int nrefl_ = (p->hdr.n_light > 0 && D > 1) ? D - 1 : 0;
+    const bool sorted = fuse_on() && !overlap && !levels && nrefl_ > 1 && p->hdr.n_tri == 0 && p->hdr.n_pl == 0 &&
+                        p->hdr.cull_ok && (sort_mode() == 2 || (sort_mode() == 1 && p->hdr.bvh_ok));
+    // dense work lists: 64 per-level record counts, per level the sort histogram, then per level the
+    // slots of its records in tile order, then (sorted) in sort-key order
+    const size_t list0 = 64 + (size_t)nlev * SORT_BINS;
+    const size_t items_ints = list0 + slots * nlev * (sorted ? 2 : 1);
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_items), &p->items_bytes, items_ints * sizeof(int), &p->gen);
-    const bool overlap = lit_overlap(p) && D > 1 && p->hdr.n_light > 0;
+    if (rc == RT_OK && sorted)
+        rc = grow(reinterpret_cast<void **>(&p->d_keyrank), &p->keyrank_bytes, slots * nlev * sizeof(int2), &p->gen);
     if (rc == RT_OK && overlap) rc = side_stream(p);
     if (rc != RT_OK) return rc;
     // the primary rays' candidate masks of the whole slab (k_pmask), recomputed only when the
@@ -2067,11 +2089,16 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         auto qk = [&](int k) { return q + (size_t)k * ntiles * TILE_SLOTS; };
         auto ck = [&](int k) { return p->d_counts + (size_t)k * ntiles; };
         int *nitems = p->d_items; // [0, 64): per-level record counts
-        auto ik = [&](int k) { return p->d_items + 64 + (size_t)k * ntiles * TILE_SLOTS; };
+        int *lists = p->d_items + list0;
+        auto ik = [&](int k) { return lists + (size_t)k * ntiles * TILE_SLOTS; };
+        auto is_sorted = [&](int k) { return sorted && k >= 1 && k < nrefl; };
+        auto hk = [&](int k) { return is_sorted(k) ? p->d_items + 64 + (size_t)k * SORT_BINS : nullptr; };
+        auto krk = [&](int k) { return is_sorted(k) ? p->d_keyrank + (size_t)k * ntiles * TILE_SLOTS : nullptr; };
+        auto sk = [&](int k) { return is_sorted(k) ? lists + (size_t)(nlev + k) * ntiles * TILE_SLOTS : ik(k); };
         auto colk = [&](int k) { return k > 0 ? p->d_colbuf + (size_t)(k - 1) * ntiles * TILE_SLOTS * 3 : nullptr; };
         auto chk = [&](int k) { return p->d_child + (size_t)k * ntiles * TILE_SLOTS; };
         auto litk = [&](int k) { return p->d_lit + (size_t)k * ntiles * TILE_SLOTS; };
-        HIPCHK(hipMemsetAsync(nitems, 0, 64 * sizeof(int), st));
+        HIPCHK(hipMemsetAsync(nitems, 0, (sorted ? list0 : 64) * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
         const PassGeom g{W, H, rb, sh, ns, row0, spp, sample, seed, acc_p}; // level-0 records are rebuilt from it
         const dim3 grid(std::min(ntiles, PRIMARY_GRID)); // k_primary: grid-stride loop over the tiles
@@ -2091,7 +2118,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         // level k's dense list, then its shading (k_light reads only level k: on a side stream
         // it starts as soon as the list exists and runs beside the next reflections)
         auto level_lists = [&](int k) -> int {
-            hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k);
+            hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k, hk(k), krk(k),
+                               sk(k));
             HIPCHK(hipGetLastError());
             if (overlap) {
                 HIPCHK(hipEventRecord(p->ev_level[k], st));
@@ -2126,8 +2154,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             if (fuse) {
 #define RT_RS(SPHV, ILPV, LDSV, BVHV)                                                                               \
     hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV>), dim3(sblocks), dim3(BLOCK), LDSV, st, rhdr,   \
-                       p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
-                       colk(k - 1), g)
+                       p->d_tab, p->d_itab, k, o, qk(k - 1), sk(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
+                       colk(k - 1), hk(k), krk(k), g)
                 // levels traversing the sphere BVH (unstaged scenes only): the BVH instantiations
                 const bool bvh_k = !staged && rhdr.bvh_ok && k >= rhdr.bvh_level;
                 if (staged && k == 1) RT_RS(2, false, lds, false);
@@ -2167,7 +2195,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             auto walk = [&](hipStream_t s_, int lo, int hi, bool deep) {
 #define RT_WALK_K(SPHV, BITSV, DEEPV, PADV, LDSV)                                                                    \
     hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV, DEEPV, PADV>), dim3(sblocks), dim3(BLOCK), LDSV, s_,       \
-                       p->hdr, p->d_tab, p->d_itab, D, o, q, ls_, p->d_items + 64, nitems, p->d_colbuf, p->d_child,  \
+                       p->hdr, p->d_tab, p->d_itab, D, o, q, ls_, lists, nitems, p->d_colbuf, p->d_child,            \
                        p->d_lit, lo, hi, g)
 #define RT_WALK(SPHV, BITSV, LDSV)                                                                                  \
     do {                                                                                                           \
@@ -2198,13 +2226,13 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             if (D > 2 && overlap) {
                 if (staged)
                     hipLaunchKernelGGL((k_walk_deep<GENPOW, 2>), dim3(sblocks), dim3(BLOCK), lds, st, p->hdr,
-                                       p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, colk(2));
+                                       p->d_tab, p->d_itab, D, q, ls_, lists, nitems, p->d_child, colk(2));
                 else if (sph_only)
                     hipLaunchKernelGGL((k_walk_deep<GENPOW, 1>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
-                                       p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, colk(2));
+                                       p->d_tab, p->d_itab, D, q, ls_, lists, nitems, p->d_child, colk(2));
                 else
                     hipLaunchKernelGGL((k_walk_deep<GENPOW, 0>), dim3(sblocks), dim3(BLOCK), 0, st, p->hdr,
-                                       p->d_tab, p->d_itab, D, q, ls_, p->d_items + 64, nitems, p->d_child, colk(2));
+                                       p->d_tab, p->d_itab, D, q, ls_, lists, nitems, p->d_child, colk(2));
                 HIPCHK(hipGetLastError());
             }
             if (overlap) {

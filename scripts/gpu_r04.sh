@@ -4,7 +4,8 @@
 #   bash scripts/gpu_r04.sh TAG suite                    the whole GPU suite
 #   bash scripts/gpu_r04.sh TAG bench [c2 c3 c3d c4 c5]  bench lines (c3d: the driver's 20/5 steps)
 #   bash scripts/gpu_r04.sh TAG ab VARIANT...            A/B of library variants (eraytracer_amd/variants/
-#                                                        librtmi355x_NAME.so via RT_LIB_PATH; "-" = the default build)
+#                                                        librtmi355x_NAME.so via RT_LIB_PATH; "-" = the default build;
+#                                                        "env:VAR=value" = the default build with that environment)
 #                                                        on configs BENCH_CFGS (default "c3 c5")
 set -o pipefail
 TAG=${1:-r04}; MODE=${2:-bench}; shift 2 || true
@@ -49,8 +50,9 @@ case $MODE in
     for rep in 1 2; do
       for c in ${BENCH_CFGS:-c3q c5q}; do
         for v in "$@"; do
-          if [ "$v" = "-" ]; then lib=""; else lib="eraytracer_amd/variants/librtmi355x_$v.so"; fi
-          RT_LIB_PATH=$lib timeout -k 10 300 python bench.py $(cfg_args $c) > gpurun_out/${TAG}_ab_one.json 2> gpurun_out/${TAG}_ab_one.err \
+          lib=""; ev=""
+          case $v in -) ;; env:*) ev=${v#env:} ;; *) lib="eraytracer_amd/variants/librtmi355x_$v.so" ;; esac
+          env $ev RT_LIB_PATH=$lib timeout -k 10 300 python bench.py $(cfg_args $c) > gpurun_out/${TAG}_ab_one.json 2> gpurun_out/${TAG}_ab_one.err \
             || { tail -5 gpurun_out/${TAG}_ab_one.err; exit 1; }
           line gpurun_out/${TAG}_ab_one.json "$c $v rep$rep" | tee -a gpurun_out/${TAG}_ab.txt || exit 1
         done
