@@ -2121,6 +2121,46 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k, hk(k), krk(k),
                                sk(k));
             HIPCHK(hipGetLastError());
+#ifdef RT_DEBUG_LISTS
+            if (is_sorted(k)) {
+                HIPCHK(hipStreamSynchronize(st));
+                int n = 0;
+                HIPCHK(hipMemcpy(&n, nitems + k, 4, hipMemcpyDeviceToHost));
+                std::vector<int> a(n), b(n), hh(SORT_BINS);
+                std::vector<int2> kr((size_t)ntiles * TILE_SLOTS);
+                HIPCHK(hipMemcpy(a.data(), ik(k), 4 * (size_t)n, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(b.data(), sk(k), 4 * (size_t)n, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(hh.data(), hk(k), 4 * SORT_BINS, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(kr.data(), krk(k), 8 * kr.size(), hipMemcpyDeviceToHost));
+                long long hs = 0;
+                for (int x : hh) hs += x;
+                std::vector<int> sa = a, sb = b;
+                std::sort(sa.begin(), sa.end());
+                std::sort(sb.begin(), sb.end());
+                {
+                    std::vector<int> cn(ntiles);
+                    HIPCHK(hipMemcpy(cn.data(), ck(k), 4 * (size_t)ntiles, hipMemcpyDeviceToHost));
+                    std::vector<HitRec> rec((size_t)ntiles * TILE_SLOTS);
+                    HIPCHK(hipMemcpy(rec.data(), qk(k), sizeof(HitRec) * rec.size(), hipMemcpyDeviceToHost));
+                    std::vector<int> seen(SORT_BINS * 64, 0);
+                    for (int x : a) {
+                        const int2 v = kr[x];
+                        const bool okk = v.x >= 0 && v.x < SORT_BINS && v.y >= 0 && v.y < hh[v.x];
+                        if (!okk || (v.y < 64 && seen[v.x * 64 + v.y]++))
+                            std::fprintf(stderr, "  level %d slot %d (tile %d cnt %d): key %d rank %d bin %d; rec pix %d obj %d parent %d\n",
+                                         k, x, x >> 8, cn[x >> 8], v.x, v.y, okk ? hh[v.x] : -1, rec[x].pix, rec[x].obj,
+                                         rec[x].parent);
+                    }
+                }
+                if (sa != sb || hs != n) {
+                    std::fprintf(stderr, "RT_DEBUG_LISTS sample %d level %d: n %d hist %lld, lists differ\n", sample, k, n, hs);
+                    for (int x : a) {
+                        if (!std::binary_search(sb.begin(), sb.end(), x))
+                            std::fprintf(stderr, "  missing slot %d key %d rank %d (bin count %d)\n", x, kr[x].x, kr[x].y, hh[kr[x].x & (SORT_BINS - 1)]);
+                    }
+                }
+            }
+#endif
             if (overlap) {
                 HIPCHK(hipEventRecord(p->ev_level[k], st));
                 HIPCHK(hipStreamWaitEvent(ls(k), p->ev_level[k], 0));
