@@ -107,16 +107,28 @@ __device__ __forceinline__ double div_n(double a, double b) {
 
 // a / n for a frame dimension n (W, H; 1 <= n <= 2^20) and 0 <= a < 2^44 exactly representable:
 // for a power of two the quotient is exact, so the correctly rounded division is the exponent
-// shift (one v_ldexp_f64 instead of v_rcp_f64 and seven fma / mul) — the same bits
+// shift (one v_ldexp_f64 instead of v_rcp_f64 and seven fma / mul) — the same bits.  n (uniform)
+// is made opaque where it is used: otherwise the compiler hoists (double) n and its reciprocal out
+// of the kernels' record loops into VGPRs that stay live (and spilled) across everything.
 __device__ __forceinline__ double div_dim(double a, int n) {
     if ((n & (n - 1)) == 0) return __builtin_amdgcn_ldexp(a, -__builtin_ctz((unsigned)n)); // (wave-uniform)
+    asm volatile("" : "+s"(n));
     return div_n(a, (double)n);
 }
 // floor(a / n) for 0 <= a < 2^31, 1 <= n <= 2^20: a shift for a power of two; otherwise the
 // correctly rounded binary64 quotient, which truncates to the exact integer quotient
 __device__ __forceinline__ int idiv_dim(int a, int n) {
     if ((n & (n - 1)) == 0) return a >> __builtin_ctz((unsigned)n); // (wave-uniform)
+    asm volatile("" : "+s"(n));
     return (int)div_n((double)a, (double)n);
+}
+// The lane's index in its wave, opaque to the optimiser: lane masks derived from it are recomputed
+// where they are used (two instructions) instead of being hoisted out of the record loops and kept
+// live — or spilled — across the shading.
+__device__ __forceinline__ int lane_id() {
+    int l = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(l));
+    return l;
 }
 
 // FAST: the caller guarantees x is in range (a sphere test's discriminant, >= 0.001 or 1.0 by
@@ -1258,7 +1270,10 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
 // re-read per light for the same reason.
 // bits (optional): bit i set where light i's shadow test passed (lights 0..31; only lanes whose
 // light term is not exactly zero are tested, the others' bits are 0 and never matter).
-template <bool GENPOW, int SPH = 0, bool NB = false>
+// OPQ (col a live value, not the background's constant): col is made opaque inside the light loop,
+// so col * refl is formed per light as written instead of being hoisted out of the loop into three
+// more live doubles (the fused kernel spilled them).
+template <bool GENPOW, int SPH = 0, bool NB = false, bool OPQ = false>
 __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D3 &hit, const D3 &N, const D3 &col,
                                     double refl, bool active, unsigned *bits = nullptr) {
     const SceneHdr &h = S.h;
@@ -1296,9 +1311,11 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
         const bool lb = lit_by<SPH, NB>(SL, i, T, D3{-ln.x, -ln.y, -ln.z}, need, hb, Lp);
         if (bits && lb && i < 32) *bits |= 1u << i;
         const double lit = lb ? 1.0 : 0.0;
-        F.x = F.x + (col.x * refl + lc.x * lit);
-        F.y = F.y + (col.y * refl + lc.y * lit);
-        F.z = F.z + (col.z * refl + lc.z * lit);
+        D3 c = col;
+        if (OPQ) asm volatile("" : "+v"(c.x), "+v"(c.y), "+v"(c.z));
+        F.x = F.x + (c.x * refl + lc.x * lit);
+        F.y = F.y + (c.y * refl + lc.y * lit);
+        F.z = F.z + (c.z * refl + lc.z * lit);
     }
     return F;
 }
@@ -1390,7 +1407,7 @@ __global__ __launch_bounds__(256, NB ? RT_FUSED_NB_WAVES : RT_WAVES_PER_SIMD) vo
                 hit_geom(SL, id, o2, d2, st[k * BLOCK + tid], hit, N);
             }
             const double refl = SL.tab[SL.h.o_obj + id * OBJ_W + 8];
-            const D3 F = shade<GENPOW, 0, NB>(SL, id, d2, hit, N, col, refl, on);
+            const D3 F = shade<GENPOW, 0, NB, true>(SL, id, d2, hit, N, col, refl, on);
             if (on) col = F;
         }
     } else {
