@@ -1362,6 +1362,12 @@ __global__ __launch_bounds__(256, NB ? RT_FUSED_NB_WAVES : RT_WAVES_PER_SIMD) vo
     if (ORDER == RT_ORDER_EXACT) {
         double *st = reinterpret_cast<double *>(smem);               // [depth][BLOCK] distances
         int *so = reinterpret_cast<int *>(smem + (size_t)depth * BLOCK * 8); // [depth][BLOCK] object ids
+        // [3][BLOCK] the primary direction, read back by each level's replay instead of being kept
+        // live (spilled) across the chain
+        double *sd0 = reinterpret_cast<double *>(smem + (size_t)depth * BLOCK * 12);
+        sd0[tid] = d0.x;
+        sd0[BLOCK + tid] = d0.y;
+        sd0[2 * BLOCK + tid] = d0.z;
         // forward: the reflection chain's nearest-object scans
         D3 o = cam, d = d0;
         bool alive = active;
@@ -1395,7 +1401,7 @@ __global__ __launch_bounds__(256, NB ? RT_FUSED_NB_WAVES : RT_WAVES_PER_SIMD) vo
             const Scene SL = fresh_scene(S); // the header re-read per level (fresh_scene)
             const int k = nlev - 1 - m;
             const bool on = k >= 0;
-            D3 o2 = cam, d2 = d0, hit = cam, N = cam;
+            D3 o2 = cam, d2 = D3{sd0[tid], sd0[BLOCK + tid], sd0[2 * BLOCK + tid]}, hit = cam, N = cam;
             int id = 0;
             if (on) {
                 for (int j = 0; j < k; ++j) { // replay the chain to level k
@@ -1442,7 +1448,13 @@ __global__ __launch_bounds__(256, NB ? RT_FUSED_NB_WAVES : RT_WAVES_PER_SIMD) vo
         }
     }
     if (!active) return; // slab rows past the image are not written
-    const size_t pix = (size_t)ly * W + x;
+    // the pixel's address recomputed from an opaque thread index rather than kept live (spilled)
+    // across the chain
+    int t2 = threadIdx.x;
+    asm volatile("" : "+v"(t2));
+    const int x2 = blockIdx.x * TILE + ((t2 >> 6) & 1) * 8 + (t2 & 7);
+    const int ly2 = row0 + blockIdx.y * TILE + ((t2 >> 6) >> 1) * 8 + ((t2 & 63) >> 3);
+    const size_t pix = (size_t)ly2 * W + x2;
     if (PREC == RT_OUT_F64) {
         double *o = reinterpret_cast<double *>(out) + pix * 3;
         o[0] = col.x; o[1] = col.y; o[2] = col.z;
@@ -1630,7 +1642,7 @@ template <int ORDER, int PREC, bool GENPOW>
 int launch_t(rt_prepared *p, int W, int H, int depth, int rb, int shard, int nshards, int row0, int row_end,
              void *out, uint8_t *levels, hipStream_t st, int levels_hit) {
     dim3 grid((W + TILE - 1) / TILE, (row_end - row0 + TILE - 1) / TILE);
-    size_t lds = ORDER == RT_ORDER_EXACT ? (size_t)depth * BLOCK * 12 : 0;
+    size_t lds = ORDER == RT_ORDER_EXACT ? (size_t)depth * BLOCK * 12 + (size_t)BLOCK * 24 : 0;
     KtScope kt(p, RT_KT_RENDER, st);
     // scenes without wave beams (few spheres, e.g. the reference's own scene) take the beam-free build
 #define RT_K_RENDER(LV, NB)                                                                                            \
