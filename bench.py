@@ -66,6 +66,9 @@ def parse():
                     help="seconds of untimed frames before the warmup steps (clock ramp; 0 = none)")
     ap.add_argument("--iso", type=int, default=20,
                     help="frames launched back to back after the timed region to time the dominant kernel alone")
+    ap.add_argument("--span-timing", action="store_true",
+                    help="also bracket the dominant kernel with HIP events inside the timed region "
+                         "(launch_span_ms_in_flight; off by default: the timed frames run as the product runs them)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-boundary", action="store_true")
     ap.add_argument("--inflight", type=int, default=None,
@@ -279,7 +282,8 @@ def main():
     # the dominant kernel's launches are bracketed by events on their own streams
     engine = engine_of(N, fr, args.spp)
     dom_label, dom_kt, dom_desc = DOMINANT[engine]
-    fr.time_kernels(getattr(N, dom_kt))
+    if args.span_timing:
+        fr.time_kernels(getattr(N, dom_kt))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
@@ -300,7 +304,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps
-    span_ms, span_n = fr.kernel_time(getattr(N, dom_kt))
+    span_ms, span_n = fr.kernel_time(getattr(N, dom_kt)) if args.span_timing else (None, 0)
     fr.time_kernels(0)
     # The dominant kernel alone: with frames in flight a launch's events also span the time it
     # queues behind other frames' kernels, so its duration is timed again over args.iso frames
@@ -332,7 +336,8 @@ def main():
         # Roofline of the dominant kernel: its executed binary64 work per launch (the FP64
         # wave-instructions the committed rocprofv3 PMC profile of this workload counts for it,
         # x 64 lanes; counts do not depend on timing) over its average launch duration measured
-        # live in the timed region (HIP events on its own stream).  Peak: 39.3 T lane-ops/s
+        # live right after the timed region (HIP events on its own stream, --iso frames launched
+        # back to back).  Peak: 39.3 T lane-ops/s
         # (78.6 TFLOP/s FP64 vector counting an FMA as 2; a wave64 FP64 op issues over 4 cycles).
         roof = {"bound": "valu", "kernel": dom_label.split("#")[0], "what": dom_desc, "peak": PEAK_FP64_VALU_TOPS,
                 "unit": "TFLOP/s", "achieved": None, "frac": None, "traffic": None,
@@ -375,9 +380,10 @@ def main():
         roof["note"] = ("FP64 VALU roofline (binding; MFMA does not apply, HBM does not bind): achieved = "
                         "the dominant kernel's executed FP64 wave-instructions per launch (rocprofv3 PMC, "
                         "profile named) x 64 lanes / its average launch duration measured live with HIP events "
-                        f"on its stream over {args.iso} frames launched back to back after the timed region (in "
-                        f"the timed region {inflight} frames in flight share the GPU and a launch's events also "
-                        "span its queueing: launch_span_ms_in_flight); launch_ms_rocprof = rocprofv3's average "
+                        f"on its stream over {args.iso} frames launched back to back after the timed region (the "
+                        "timed region itself carries no kernel events; with --span-timing, launch_span_ms_in_flight "
+                        f"= the same launches timed among {inflight} frames in flight, queueing included); "
+                        "launch_ms_rocprof = rocprofv3's average "
                         "duration of the same launches; traffic = that kernel's HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE). "
                         "valu_issue_frac: the same kernel's VALU issue cycles (FP64 wave-instructions x 4, other VALU x 2) / "
                         "(1024 SIMDs x 2.4 GHz x launch time) - the beam and BVH filters run in binary32, so the FP64 fraction "
