@@ -1972,12 +1972,15 @@ bool fuse_on() {
     return on;
 }
 
-// Sorted deep levels (SORT_BINS): RT_SORT=0 off, 1 (default) scenes with the sphere BVH (many
-// spheres: incoherent deep levels), 2 every spheres-only scene — for A/B runs.
+// Sorted deep levels (SORT_BINS): RT_SORT=0 off (default), 1 scenes with the sphere BVH (many
+// spheres: incoherent deep levels), 2 every spheres-only scene — for A/B runs.  Measured round 4
+// (config 5, kernels alone per sample pass): the BVH levels 2-7 got 7 % faster (1,135 -> 1,067 us)
+// but the sorted lists' scattered writes made k_items 6x slower (+320 us) and the producer's keys
+// cost +30 us — config 5 32.0 -> 32.4 ms per frame; config 3 (RT_SORT=2) -2 %.  Not on by default.
 int sort_mode() {
     static const int m = [] {
         const char *e = std::getenv("RT_SORT");
-        return e ? std::atoi(e) : 1;
+        return e ? std::atoi(e) : 0;
     }();
     return m;
 }
