@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-3 evidence on one MI355X, in two gpurun calls (each under gpurun's 1200 s limit):
-#   bash scripts/gpu_r03_evidence.sh TAG a   GPU parity suite + bench lines of configs 1-5
-#   bash scripts/gpu_r03_evidence.sh TAG b   rocprofv3 kernel trace + PMC passes of configs 3, 2, 5
+# Round-4 evidence on one MI355X, in two gpurun calls (each under gpurun's 1200 s limit):
+#   bash scripts/gpu_r04_evidence.sh TAG a   GPU parity suite + bench lines of configs 1-5
+#   bash scripts/gpu_r04_evidence.sh TAG b   rocprofv3 kernel trace + PMC passes of configs 3, 2, 5
 set -o pipefail
-TAG=${1:-r03}
+TAG=${1:-r04}
 PART=${2:-a}
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
@@ -16,6 +16,7 @@ if [ "$PART" = a ]; then
   b() { name=$1; shift; timeout -k 10 300 python bench.py "$@" > gpurun_out/${TAG}_bench_$name.json 2> gpurun_out/${TAG}_bench_$name.err || { tail -5 gpurun_out/${TAG}_bench_$name.err; exit 1; }; python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], 'Mpx/s', d['ms_per_step'], 'ms/frame')" gpurun_out/${TAG}_bench_$name.json $name; }
   timeout -k 10 200 python scripts/cpu_config1.py > gpurun_out/${TAG}_cfg1.json && cat gpurun_out/${TAG}_cfg1.json || exit 1
   b c3 || exit 1
+  b c3d --steps 20 --warmup 5 --no-boundary --no-cpu-baseline || exit 1
   b c2 $C2 --no-cpu-baseline || exit 1
   b c4 --size 8192 --no-cpu-baseline --no-boundary || exit 1
   b c5 $C5 --steps 10 --warmup 4 --no-boundary --cpu-seconds 10 || exit 1
