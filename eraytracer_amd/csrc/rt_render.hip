@@ -93,6 +93,35 @@ __device__ __forceinline__ double sqrt_n(double x) {
     return __builtin_fma(d, h, g);
 }
 
+// 1 / sqrt(x) as normalize/1 computes it (:554-560): Mag = sqrt(x) rounded, then 1/Mag rounded —
+// the same two correctly rounded results as sqrt_n and div_n(1, .), but the reciprocal starts from
+// the square root's own half-reciprocal h (2h = 1/sqrt(x) to ~2^-46 after sqrt_n's Goldschmidt
+// step) instead of a fresh v_rcp_f64 and two Newton steps: one Newton step makes it faithful, and
+// the final correction step (div_n's last) rounds it correctly.  For x in [SQRT_N_LO, SQRT_N_HI]
+// with sqrt(x) in [RCP_N_LO, RCP_N_HI]; rt_selftest_math checks it bit for bit against the
+// library's sqrt and division.
+#ifndef RT_RCP_FROM_SQRT
+#define RT_RCP_FROM_SQRT 1
+#endif
+__device__ __forceinline__ double rsqrt_n(double x) {
+    const double s = __builtin_amdgcn_rsq(x);
+    double g = x * s;
+    double h = s * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    const double m = __builtin_fma(d, h, g); // == sqrt_n(x)
+    double y = h + h;                        // exact
+    const double e = __builtin_fma(-m, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    const double q = 1.0 * y;
+    const double rr = __builtin_fma(-m, q, 1.0);
+    return __builtin_fma(rr, y, q);
+}
+
 // a / b for |b| in [RCP_N_LO, RCP_N_HI] and |a| small enough that a/b is a normal number or 0
 __device__ __forceinline__ double div_n(double a, double b) {
     double y = __builtin_amdgcn_rcp(b);
@@ -147,7 +176,7 @@ __device__ __forceinline__ double sqrt_x(double x) { // == sqrt(x)
 __device__ __forceinline__ D3 normalize3(const D3 &v, bool fast = false) { // vector_normalize/1 (:554-560)
     const double m2 = v.x * v.x + v.y * v.y + v.z * v.z;
     if (fast || __ballot(!(m2 >= RCP_N_LO && m2 <= RCP_N_HI)) == 0) { // mag and 1/mag in range, mag != 0
-        const double s = div_n(1.0, sqrt_n(m2));
+        const double s = RT_RCP_FROM_SQRT ? rsqrt_n(m2) : div_n(1.0, sqrt_n(m2));
         return D3{v.x * s, v.y * s, v.z * s};
     }
     double mag = sqrt(m2);
@@ -1479,6 +1508,10 @@ __global__ __launch_bounds__(256) void k_selftest_math(unsigned long long n, uns
         const long long e = 1023 - 767 + (long long)((r >> 52) % (767 + 1000));
         const double x = __longlong_as_double((long long)((unsigned long long)e << 52 | (r & 0xFFFFFFFFFFFFFull)));
         if (__double_as_longlong(sqrt_n(x)) != __double_as_longlong(sqrt(x))) ++local;
+        // 1 / sqrt(y) over normalize3's fast range [2^-400, 2^400] (Mag and its reciprocal in range)
+        const long long ey = 1023 - 400 + (long long)((r >> 52) % 800);
+        const double yv = __longlong_as_double((long long)((unsigned long long)ey << 52 | (r & 0xFFFFFFFFFFFFFull)));
+        if (__double_as_longlong(rsqrt_n(yv)) != __double_as_longlong(1.0 / sqrt(yv))) ++local;
         // 1/b and a/b: b over [2^-400, 2^400], a an integer below 2^21 (the primary-ray divisions)
         const long long eb = 1023 - 400 + (long long)((r2 >> 52) % 800);
         const double b = __longlong_as_double((long long)((unsigned long long)eb << 52 | (r2 & 0xFFFFFFFFFFFFFull)));
