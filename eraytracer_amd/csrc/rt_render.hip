@@ -1307,7 +1307,6 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
                                     double refl, bool active, unsigned *bits = nullptr) {
     const SceneHdr &h = S.h;
     if (__ballot(active) == 0) return D3{0.0, 0.0, 0.0}; // no hit to shade in this wave
-    const double *m = obj_row<SPH>(S, id);
     const Target T = make_target<SPH>(S, id, active);
     // the hit ball is only needed for non-sphere shadow targets (see lit_by)
     HitBall hb;
@@ -1319,6 +1318,11 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
     for (int i = 0; i < h.n_light; ++i) {
         const Scene &SL = S; // (re-reading the header per light, fresh_scene: measured neutral)
         const double *L = SL.tab + SL.h.o_light + i * LIGHT_W;
+        // the material row's address formed per light from the (opaque) object id: one live
+        // register instead of a 64-bit pointer across the loop
+        int idl = id;
+        asm volatile("" : "+v"(idl));
+        const double *m = obj_row<SPH>(S, idl);
         const D3 Lc = {L[0], L[1], L[2]}, Lp = {L[3], L[4], L[5]}, Sc = {L[6], L[7], L[8]};
         const double2 m34 = *reinterpret_cast<const double2 *>(m + 4), m67 = *reinterpret_cast<const double2 *>(m + 6);
         const D3 mc = {m[3], m34.x, m34.y};
