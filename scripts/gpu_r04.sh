@@ -47,7 +47,7 @@ case $MODE in
     done ;;
   ab)
     : > gpurun_out/${TAG}_ab.txt
-    for rep in 1 2; do
+    for rep in $(seq 1 ${REPS:-2}); do
       for c in ${BENCH_CFGS:-c3q c5q}; do
         for v in "$@"; do
           lib=""; ev=""
