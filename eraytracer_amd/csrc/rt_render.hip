@@ -100,8 +100,11 @@ __device__ __forceinline__ double sqrt_n(double x) {
 // the final correction step (div_n's last) rounds it correctly.  For x in [SQRT_N_LO, SQRT_N_HI]
 // with sqrt(x) in [RCP_N_LO, RCP_N_HI]; rt_selftest_math checks it bit for bit against the
 // library's sqrt and division.
+// Off: bit-identical to the library on 1.3e10 random operands (rt_selftest_math), yet the default
+// scene's frames differed from the oracle in 2.5 % of their pixels (<= 1.3e-14): some structured
+// operands (integer scene coordinates) round differently.  Kept for study.
 #ifndef RT_RCP_FROM_SQRT
-#define RT_RCP_FROM_SQRT 1
+#define RT_RCP_FROM_SQRT 0
 #endif
 __device__ __forceinline__ double rsqrt_n(double x) {
     const double s = __builtin_amdgcn_rsq(x);
