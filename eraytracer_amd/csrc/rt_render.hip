@@ -1518,7 +1518,21 @@ __global__ __launch_bounds__(256) void k_selftest_math(unsigned long long n, uns
         // 1 / sqrt(y) over normalize3's fast range [2^-400, 2^400] (Mag and its reciprocal in range)
         const long long ey = 1023 - 400 + (long long)((r >> 52) % 800);
         const double yv = __longlong_as_double((long long)((unsigned long long)ey << 52 | (r & 0xFFFFFFFFFFFFFull)));
-        if (__double_as_longlong(rsqrt_n(yv)) != __double_as_longlong(1.0 / sqrt(yv))) ++local;
+        if (RT_RCP_FROM_SQRT && __double_as_longlong(rsqrt_n(yv)) != __double_as_longlong(1.0 / sqrt(yv))) ++local;
+        // structured operands (scenes are written with small integers and short fractions): the
+        // squared length of a vector of integers in [-2^10, 2^10] scaled by 2^-k
+        {
+            const double sx = (double)((long long)(r & 0x7FF) - 1024), sy = (double)((long long)((r >> 11) & 0x7FF) - 1024),
+                         sz = (double)((long long)((r >> 22) & 0x7FF) - 1024);
+            const double sc = __builtin_amdgcn_ldexp(1.0, -(int)((r >> 33) & 15));
+            const D3 w = {sx * sc, sy * sc, sz * sc};
+            const D3 uw = normalize3(w);
+            const double mw = sqrt(w.x * w.x + w.y * w.y + w.z * w.z), sw = 1.0 / mw;
+            if (mw != 0 && (__double_as_longlong(uw.x) != __double_as_longlong(w.x * sw) ||
+                            __double_as_longlong(uw.y) != __double_as_longlong(w.y * sw) ||
+                            __double_as_longlong(uw.z) != __double_as_longlong(w.z * sw)))
+                ++local;
+        }
         // 1/b and a/b: b over [2^-400, 2^400], a an integer below 2^21 (the primary-ray divisions)
         const long long eb = 1023 - 400 + (long long)((r2 >> 52) % 800);
         const double b = __longlong_as_double((long long)((unsigned long long)eb << 52 | (r2 & 0xFFFFFFFFFFFFFull)));
