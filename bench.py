@@ -343,7 +343,7 @@ def main():
                 "unit": "TFLOP/s", "achieved": None, "frac": None, "traffic": None,
                 "launch_ms_live": round(dom_ms, 4) if dom_ms else None, "launches_timed": dom_n,
                 "launch_span_ms_in_flight": round(span_ms, 4) if span_ms else None}
-        frame_exec = valu_busy = traffic_frame = None
+        frame_exec = valu_busy = traffic_frame = traffic_frame_low = None
         if prof:
             d, path = prof
             kd = d.get("kernels", {}).get(dom_label, {})
@@ -359,8 +359,9 @@ def main():
                     roof["valu_issue_frac"] = round((4 * f64 + 2 * (valu - f64)) / (1024 * 2.4e9 * dom_ms / 1e3), 4)
                     roof["valu_wave_insts_per_launch"] = round(valu)
             kc = kd.get("counters", {})
-            if "FETCH_SIZE" in kc and "WRITE_SIZE" in kc:  # KiB; FETCH x2 on gfx950 (MI355X_MICROARCH.md)
+            if "FETCH_SIZE" in kc and "WRITE_SIZE" in kc:  # KiB; reads between FETCH x1 (gathers) and x2 (streams)
                 roof["traffic"] = round((2 * kc["FETCH_SIZE"] + kc["WRITE_SIZE"]) * 1024)
+                roof["traffic_low"] = round((kc["FETCH_SIZE"] + kc["WRITE_SIZE"]) * 1024)
             if kd.get("isolated_avg_ns"):
                 roof["launch_ms_rocprof"] = round(kd["isolated_avg_ns"] / 1e6, 4)
             if kd.get("avg_ns"):
@@ -374,6 +375,8 @@ def main():
                 valu_busy = (4 * f64f + 2 * (c["SQ_INSTS_VALU"] * per - f64f)) / (1024 * 2.4e9 * k_s)
             if d.get("hbm_bytes_per_launch") is not None:
                 traffic_frame = d["hbm_bytes_per_launch"] * per
+            if d.get("hbm_bytes_per_launch_low") is not None:
+                traffic_frame_low = d["hbm_bytes_per_launch_low"] * per
         roof["frame_f64_issue_frac"] = round(frame_exec, 4) if frame_exec is not None else None
         roof["frame_valu_busy_frac"] = round(valu_busy, 4) if valu_busy is not None else None
         roof["ref_work_tops"] = round(ops_rank / k_s / 1e12, 3)
@@ -384,7 +387,9 @@ def main():
                         "timed region itself carries no kernel events; with --span-timing, launch_span_ms_in_flight "
                         f"= the same launches timed among {inflight} frames in flight, queueing included); "
                         "launch_ms_rocprof = rocprofv3's average "
-                        "duration of the same launches; traffic = that kernel's HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE). "
+                        "duration of the same launches; traffic = that kernel's HBM bytes per launch, reads counted "
+                        "as FETCH_SIZE x2 (upper bound: exact for coalesced streams) + WRITE_SIZE, traffic_low with "
+                        "FETCH_SIZE x1 (exact for 8-64 B gathers; scripts/hbm_calib.hip). "
                         "valu_issue_frac: the same kernel's VALU issue cycles (FP64 wave-instructions x 4, other VALU x 2) / "
                         "(1024 SIMDs x 2.4 GHz x launch time) - the beam and BVH filters run in binary32, so the FP64 fraction "
                         "alone understates how busy the VALU is. frame_f64_issue_frac / frame_valu_busy_frac: "
@@ -417,8 +422,11 @@ def main():
             "roofline": roof,
             "roofline_hbm": {"bound": "hbm", "achieved": round(hbm_ach, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": round(hbm_ach / PEAK_HBM_GBS, 6), "traffic": traffic_frame,
+                             "traffic_low": traffic_frame_low,
                              "note": "algorithmic bytes: the framebuffer store (12 B/px f32, 24 f64) per GPU time per "
-                                     "frame; traffic = measured HBM bytes per frame launch (PMC)"},
+                                     "frame; traffic = measured HBM bytes per frame launch (PMC; reads as FETCH_SIZE x2, the "
+                                     "upper bound), traffic_low = the same with FETCH_SIZE x1 (lower bound; "
+                                     "profiles/r04_hbm_calib.txt)"},
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_max_rank": round(kern_ms_max, 4),
             "kernel_mpx_s": round(px_rank / k_s / 1e6, 3),

@@ -13,9 +13,13 @@ entries are labelled name#i, i = occurrence within the frame (k_reflect#0 makes 
 k_shade#0 shades the DEEPEST level).
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB and come from
-separate passes.  FETCH_SIZE under-reports wide coalesced streaming reads by 2x on gfx950; the
-hit-record queues are read with 64-B-per-lane loads, so the read side is reported raw and
-doubled (fetch_bytes_corrected); WRITE_SIZE is reported raw.
+separate passes.  Calibrated here (scripts/hbm_calib.hip, profiles/r04_hbm_calib.txt): a coalesced
+16-B-per-lane stream moves 128-B lines and FETCH_SIZE reports half of its bytes; a random gather of
+64, 16 or 8 bytes per lane moves one 64-B request per lane and FETCH_SIZE reports exactly that.
+The engine's kernels mix both, so a kernel's read bytes lie between the raw FETCH_SIZE (lower
+bound, exact for gathers) and twice it (fetch_bytes_corrected, upper bound, exact for streams);
+both are reported (hbm_bytes_per_launch = upper, hbm_bytes_per_launch_low = lower).  WRITE_SIZE is
+reported raw.
 """
 import csv
 import glob
@@ -177,10 +181,12 @@ def main():
     dd = out["derived"]
     if "fetch_bytes" in dd:
         out["hbm_bytes_per_launch"] = dd["fetch_bytes_corrected"] + dd["write_bytes"]
+        out["hbm_bytes_per_launch_low"] = dd["fetch_bytes"] + dd["write_bytes"]
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
-    print(json.dumps({"trace": tr, "derived": dd, "hbm_bytes_per_launch": out.get("hbm_bytes_per_launch")},
+    print(json.dumps({"trace": tr, "derived": dd, "hbm_bytes_per_launch": out.get("hbm_bytes_per_launch"),
+                      "hbm_bytes_per_launch_low": out.get("hbm_bytes_per_launch_low")},
                      indent=1))
     for lab, e in out["kernels"].items():
         x = e["derived"]
