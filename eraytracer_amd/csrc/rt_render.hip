@@ -2039,6 +2039,27 @@ int sort_mode() {
     return m;
 }
 
+// RT_MISS_MEMSET=1: spp = 1 passes zero their image rows with a fill before k_primary, which then
+// skips the misses' pixels (A/B).
+bool miss_memset_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("RT_MISS_MEMSET");
+        return e && std::strcmp(e, "1") == 0;
+    }();
+    return on;
+}
+
+// The slab rows of shard sh that lie inside the image (a prefix of the slab).
+size_t valid_slab_rows(int H, int rb, int sh, int ns) {
+    const size_t slab = rt_shard_rows((uint32_t)H, (uint32_t)rb, (uint32_t)ns);
+    size_t v = 0;
+    for (size_t blk = 0; blk * rb < slab; ++blk) {
+        const long long base = ((long long)blk * ns + sh) * rb;
+        v += (size_t)std::max(0LL, std::min((long long)rb, (long long)H - base));
+    }
+    return v;
+}
+
 // Does a wavefront pass write every pixel exactly once?  Yes with k_reflect_shade (the colours of
 // records with a reflection hit are left to k_walk) and without reflections; no when k_light
 // shades level 0 provisionally beside the chain (side streams, or levels requested).
@@ -2190,14 +2211,24 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         const dim3 grid(std::min(ntiles, PRIMARY_GRID)); // k_primary: grid-stride loop over the tiles
         {
             KtScope kt(p, RT_KT_PRIMARY, st);
+            // RT_MISS_MEMSET=1 (A/B): the pass's image rows zeroed by a fill (streamed full lines),
+            // k_primary then writes only hits' records, not the misses' scattered 12-byte pixels
+            int preset = 0;
+            if (miss_memset_on() && acc_p == nullptr) {
+                const int valid = (int)std::min<size_t>((size_t)rows, valid_slab_rows(H, rb, sh, ns) > (size_t)row0
+                                                                           ? valid_slab_rows(H, rb, sh, ns) - row0 : 0);
+                if (valid > 0)
+                    HIPCHK(hipMemsetAsync(o, 0, (size_t)valid * W * 3 * (PREC == RT_OUT_F64 ? 8 : 4), st));
+                preset = 1;
+            }
             if (lv0)
                 hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W,
                                    H, D, rb, sh, ns, rows, row0, o, lv0, q, p->d_counts, ntiles, spp, sample, seed, acc_p,
-                                   pmask);
+                                   pmask, preset);
             else
                 hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
                                    W, H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed, acc_p,
-                                   pmask);
+                                   pmask, preset);
         }
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));

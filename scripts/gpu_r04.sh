@@ -19,6 +19,9 @@ cfg_args() {
     c3) echo "" ;;
     c3d) echo "--steps 20 --warmup 5" ;;
     c3q) echo "--no-cpu-baseline --no-boundary" ;;
+    c3q3) echo "--no-cpu-baseline --no-boundary --inflight 3" ;;
+    c3q6) echo "--no-cpu-baseline --no-boundary --inflight 6" ;;
+    c3dq) echo "--steps 20 --warmup 5 --no-cpu-baseline --no-boundary" ;;
     c4) echo "--size 8192 --no-cpu-baseline --no-boundary" ;;
     c5) echo "$C5 --steps 10 --warmup 4 --no-boundary --cpu-seconds 10" ;;
     c5q) echo "$C5 --steps 8 --warmup 3 --no-boundary --no-cpu-baseline" ;;
