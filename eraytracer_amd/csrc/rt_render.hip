@@ -2179,7 +2179,14 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         rhdr.l_stack = (int)lds_bvh;
         lds_bvh += (size_t)BLOCK * rhdr.bvh_depth * sizeof(unsigned);
     }
-    auto lds_r = [&](int k) { return !staged && rhdr.bvh_ok && k >= rhdr.bvh_level ? lds_bvh : lds; };
+    // RT_BVH_STAGED=1 (A/B; with RT_BVH_MIN below the scene's sphere count): the BVH levels of an
+    // LDS-staged scene traverse it too, its nodes, rows and stacks placed after the staged tables
+    static const bool bvh_staged = [] {
+        const char *e = std::getenv("RT_BVH_STAGED");
+        return e && std::strcmp(e, "1") == 0;
+    }();
+    auto bvh_at = [&](int k) { return (!staged || bvh_staged) && rhdr.bvh_ok && k >= rhdr.bvh_level; };
+    auto lds_r = [&](int k) { return bvh_at(k) ? lds_bvh : lds; };
     // no side streams (frames in flight): each level's shading fused into the next reflection
     // pass (k_reflect_shade)
     const bool fuse = fuse_on() && !overlap && !levels && nrefl > 0;
@@ -2314,8 +2321,9 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                        p->d_tab, p->d_itab, k, o, qk(k - 1), sk(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
                        colk(k - 1), hk(k), krk(k), g)
                 // levels traversing the sphere BVH (unstaged scenes only): the BVH instantiations
-                const bool bvh_k = !staged && rhdr.bvh_ok && k >= rhdr.bvh_level;
-                if (staged && k == 1) RT_RS(2, false, lds, false);
+                const bool bvh_k = bvh_at(k);
+                if (staged && bvh_k) RT_RS(2, true, lds_r(k), true);
+                else if (staged && k == 1) RT_RS(2, false, lds, false);
                 else if (staged) RT_RS(2, true, lds, false);
                 else if (sph_only && bvh_k) RT_RS(1, true, lds_r(k), true);
                 else if (sph_only && k == 1) RT_RS(1, false, lds, false);

@@ -54,7 +54,7 @@ case $MODE in
       for c in ${BENCH_CFGS:-c3q c5q}; do
         for v in "$@"; do
           lib=""; ev=""
-          case $v in -) ;; env:*) ev=${v#env:} ;; *) lib="eraytracer_amd/variants/librtmi355x_$v.so" ;; esac
+          case $v in -) ;; env:*) ev=$(echo ${v#env:} | tr , " ") ;; *) lib="eraytracer_amd/variants/librtmi355x_$v.so" ;; esac
           env $ev RT_LIB_PATH=$lib timeout -k 10 300 python bench.py $(cfg_args $c) > gpurun_out/${TAG}_ab_one.json 2> gpurun_out/${TAG}_ab_one.err \
             || { tail -5 gpurun_out/${TAG}_ab_one.err; exit 1; }
           line gpurun_out/${TAG}_ab_one.json "$c $v rep$rep" | tee -a gpurun_out/${TAG}_ab.txt || exit 1
