@@ -377,11 +377,13 @@ __device__ __forceinline__ void stage_tables(const Scene &S) {
 }
 
 // Diagnostic build only (-DRT_STATS): per-wave event counters read back with rt_debug_stats().
+#define RT_NSTATS 20
 #ifdef RT_STATS
-__device__ unsigned long long g_stats[16];
+__device__ unsigned long long g_stats[RT_NSTATS];
 #define RT_STAT(i, v)                                                                                              \
     do {                                                                                                           \
-        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(&g_stats[i], (unsigned long long)(v));   \
+        const unsigned long long v_ = (v);                                                                         \
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(&g_stats[i], v_);                          \
     } while (0)
 #else
 #define RT_STAT(i, v) \
@@ -390,7 +392,7 @@ __device__ unsigned long long g_stats[16];
 #endif
 enum { ST_WAVES, ST_NEAR_PRE, ST_NEAR_PRE_CAND, ST_NEAR_GEN, ST_NEAR_GEN_CAND, ST_SHADOW, ST_SHADOW_CAND,
        ST_SHADOW_ITER, ST_SHADE, ST_SHADOW_CONE_ON, ST_BEAM_ON, ST_SHADOW_LANES, ST_NEAR_LANES, ST_BVH_SCANS,
-       ST_BVH_ITER, ST_BVH_LEAF };
+       ST_BVH_ITER, ST_BVH_LEAF, ST_BVH_ITER_LANES, ST_BVH_LEAF_LANES };
 
 // ---- Beam culling ----------------------------------------------------------------------------
 // A wave's 64 rays are coherent (an 8x8 pixel tile; shadow rays of one light; their
@@ -877,6 +879,7 @@ __device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &
     // expressions)
     auto leaf = [&](int k, int id) {
         RT_STAT(ST_BVH_LEAF, 1);
+        RT_STAT(ST_BVH_LEAF_LANES, __popcll(__ballot(1)));
         const double2 c01 = rows[k * 2], c2r = rows[k * 2 + 1];
         const D3 oc = {o.x - c01.x, o.y - c01.y, o.z - c2r.x};
         const double B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
@@ -890,39 +893,58 @@ __device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &
     };
     int node = act ? 0 : -1, sp = 0;
     RT_STAT(ST_BVH_SCANS, 1);
-    while (node >= 0) {
+    // the next node from the stack: the nearest pushed entry not beyond tlim (-1: traversal done)
+    auto pop = [&]() {
+        node = -1;
+        while (sp > 0) {
+            const unsigned en = stk[--sp * 64];
+            if (__uint_as_float(en & 0xffff0000u) <= tlim) {
+                node = (int)(en & 0xffffu);
+                break;
+            }
+        }
+    };
+    // one visit of `node`: both children's boxes tested; the leaves among those hit are returned
+    // in l0 / l1, the nearer inner child hit becomes `node` (the farther one pushed), else -1
+    auto visit = [&](bool &l0, bool &l1, float4 &e) {
         RT_STAT(ST_BVH_ITER, 1);
-        const float4 a = nodes[node * 4], b = nodes[node * 4 + 1], c = nodes[node * 4 + 2], e = nodes[node * 4 + 3];
+        RT_STAT(ST_BVH_ITER_LANES, __popcll(__ballot(1)));
+        const float4 a = nodes[node * 4], b = nodes[node * 4 + 1], c = nodes[node * 4 + 2];
+        e = nodes[node * 4 + 3];
         float tn0, tn1;
         bool h0, h1;
         bvh_slab2(ray, a, b, c, tlim, h0, tn0, h1, tn1);
         const int c0 = __float_as_int(e.x), c1 = __float_as_int(e.y);
-        if (h0 && c0 < 0) {
-            leaf(~c0, __float_as_int(e.z));
-            h0 = false;
-        }
-        if (h1 && c1 < 0) {
-            leaf(~c1, __float_as_int(e.w));
-            h1 = false;
-        }
+        l0 = h0 && c0 < 0;
+        l1 = h1 && c1 < 0;
+        h0 = h0 && !l0;
+        h1 = h1 && !l1;
         if (h0 && h1) {
             const bool f0 = tn0 <= tn1;
             const float tf = f0 ? tn1 : tn0;
             stk[sp * 64] = (__float_as_uint(tf) & 0xffff0000u) | (unsigned)(f0 ? c1 : c0); // tf >= 0: truncation rounds down
             ++sp;
             node = f0 ? c0 : c1;
-        } else if (h0 | h1) {
-            node = h0 ? c0 : c1;
         } else {
-            node = -1;
-            while (sp > 0) {
-                const unsigned en = stk[--sp * 64];
-                if (__uint_as_float(en & 0xffff0000u) <= tlim) {
-                    node = (int)(en & 0xffffu);
-                    break;
-                }
-            }
+            node = (h0 | h1) ? (h0 ? c0 : c1) : -1;
         }
+    };
+    // the leaves a visit returned, child 0's first: one divergent leaf test for every lane with a
+    // leaf, a second only for the lanes with two.  (Postponing a lane's leaves until half of the
+    // wave's unfinished lanes hold some, so that they are tested together, halved the leaf tests
+    // per wave but added visits: config 5 +2 % per frame, not kept.)
+    auto leaves = [&](bool l0, bool l1, const float4 &e) {
+        if (l0 | l1) {
+            leaf(~__float_as_int(l0 ? e.x : e.y), __float_as_int(l0 ? e.z : e.w));
+            if (l0 & l1) leaf(~__float_as_int(e.y), __float_as_int(e.w));
+        }
+    };
+    while (node >= 0) {
+        bool l0, l1;
+        float4 e;
+        visit(l0, l1, e);
+        leaves(l0, l1, e);
+        if (node < 0) pop();
     }
 }
 
@@ -1722,11 +1744,11 @@ extern "C" {
 #ifdef RT_STATS
 // diagnostic builds only (not part of include/rt_mi355x.h)
 int rt_debug_stats(unsigned long long *out, int n, int reset) {
-    if (n > 16) n = 16;
+    if (n > RT_NSTATS) n = RT_NSTATS;
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), n * sizeof(unsigned long long)));
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[RT_NSTATS] = {0};
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof(z)));
     }
     return RT_OK;
