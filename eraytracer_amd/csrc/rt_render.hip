@@ -1588,7 +1588,7 @@ struct rt_prepared {
     // wavefront-engine work space, grown on demand (one rt_launch in flight per rt_prepared)
     void *d_queue = nullptr;  // HitRec[slab pixels * depth]
     size_t queue_bytes = 0;
-    double *d_colbuf = nullptr; // colours of levels 1 .. depth-1, 3 doubles per slot
+    double *d_colbuf = nullptr; // colours of levels 1 .. depth-1, COL_W doubles per slot
     uint8_t *d_child = nullptr; // per level and slot: the record's reflection hit something
     size_t child_bytes = 0;
     unsigned *d_lit = nullptr;  // per level and slot: shadow answers of lights 0..31 (k_light)
@@ -2112,9 +2112,9 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     const size_t max_tiles = (size_t)tiles_x * ((pass_rows + TILE - 1) / TILE);
     const size_t slots = max_tiles * TILE_SLOTS; // per level
     int rc = grow(&p->d_queue, &p->queue_bytes, slots * nlev * sizeof(HitRec), &p->gen);
-    // colours of levels 1 .. depth-1, 3 doubles per slot (level 0 goes straight to the
+    // colours of levels 1 .. depth-1, COL_W doubles per slot (level 0 goes straight to the
     // frame), and per level the has-a-child flags
-    const size_t col_doubles = slots * 3 * (size_t)std::max(1, nlev - 1);
+    const size_t col_doubles = slots * COL_W * (size_t)std::max(1, nlev - 1);
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_colbuf), &p->colbuf_bytes, col_doubles * sizeof(double), &p->gen);
     if (rc == RT_OK) rc = grow(reinterpret_cast<void **>(&p->d_child), &p->child_bytes, slots * nlev, &p->gen);
@@ -2231,7 +2231,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         auto hk = [&](int k) { return is_sorted(k) ? p->d_items + 64 + (size_t)k * SORT_BINS : nullptr; };
         auto krk = [&](int k) { return is_sorted(k) ? p->d_keyrank + (size_t)k * ntiles * TILE_SLOTS : nullptr; };
         auto sk = [&](int k) { return is_sorted(k) ? lists + (size_t)(nlev + k) * ntiles * TILE_SLOTS : ik(k); };
-        auto colk = [&](int k) { return k > 0 ? p->d_colbuf + (size_t)(k - 1) * ntiles * TILE_SLOTS * 3 : nullptr; };
+        auto colk = [&](int k) { return k > 0 ? p->d_colbuf + (size_t)(k - 1) * ntiles * TILE_SLOTS * COL_W : nullptr; };
         auto chk = [&](int k) { return p->d_child + (size_t)k * ntiles * TILE_SLOTS; };
         auto litk = [&](int k) { return p->d_lit + (size_t)k * ntiles * TILE_SLOTS; };
         HIPCHK(hipMemsetAsync(nitems, 0, (sorted ? list0 : 64) * sizeof(int), st));
