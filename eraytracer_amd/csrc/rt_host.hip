@@ -43,6 +43,17 @@ size_t band_bytes() {
     }();
     return b;
 }
+// Test hook: RT_DEVICE_ALIAS=N makes rt_render see N devices that are all device first_dev, so
+// its multi-device path (a context, work space and band pipeline per device, every device's
+// slabs scattered into the one frame) runs on a one-GPU machine (0, the default: off)
+int device_alias() {
+    static const int n = [] {
+        const char *e = std::getenv("RT_DEVICE_ALIAS");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 && v <= RT_CTX_PER_DEVICE ? v : 0;
+    }();
+    return n;
+}
 // DMA queues a pinned frame's band copies alternate over (RT_COPY_STREAMS = 1, the default, or 2)
 int copy_streams() {
     static const int n = [] {
@@ -491,6 +502,11 @@ int rt_render(const rt_elem *scene, uint32_t n, uint32_t width, uint32_t height,
     if (rc != RT_OK) return rc;
     int navail = 0;
     if (hipGetDeviceCount(&navail) != hipSuccess || navail <= 0) return RT_ENODEV;
+    const int alias = device_alias();
+    if (alias > 0) {
+        if (o.first_dev < 0 || o.first_dev >= navail) return RT_ENODEV;
+        navail = o.first_dev + alias;
+    }
     if (o.ndev < 0) o.ndev = navail - o.first_dev;
     if (o.first_dev < 0 || o.ndev <= 0 || o.first_dev + o.ndev > navail) return RT_ENODEV;
     const uint32_t ns = o.nshards ? o.nshards : (uint32_t)o.ndev, rb = o.row_block;
@@ -519,7 +535,7 @@ int rt_render(const rt_elem *scene, uint32_t n, uint32_t width, uint32_t height,
     int err = RT_OK;
     auto shards_of = [&](uint32_t d) { return (ns - d + nd - 1) / nd; }; // shards d, d + nd, ...
     for (uint32_t d = 0; d < nd && err == RT_OK; ++d) {
-        const int dev = o.first_dev + (int)d;
+        const int dev = alias > 0 ? o.first_dev : o.first_dev + (int)d;
         err = rt_ctx_acquire(dev, scene, n, &ctx[d]);
         if (err != RT_OK) break;
         rt_ctx *c = ctx[d];

@@ -115,6 +115,42 @@ def test_distributed_shards_on_one_device(oracle, rb):
     assert np.abs(one - ref).max() <= 1e-5
 
 
+def test_multi_device_path_through_device_aliases():
+    """rt_render's multi-device loop (rt_host.hip: one context, work space and band pipeline per
+    device, each device's shards scattered into the one frame; raytracer.erl:121-149) on a
+    one-GPU machine: RT_DEVICE_ALIAS=N (a test hook read once per process, so in a child process)
+    makes the N devices all device 0.  ndev 2 and 3 with 2, 3 and 5 shards, pinned and pageable,
+    f64 and f32, with levels and supersampling, equal the one-device frames bit for bit."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r"""
+import numpy as np
+from eraytracer_amd import _native as N, scenes
+from eraytracer_amd.raytracer import render
+scene = scenes.s64()
+w, h, d = 300, 203, 5
+for prec in ("f64", "f32"):
+    one, lv1 = render(w, h, scene, d, levels=True, precision=prec)
+    iv = np.int64 if prec == "f64" else np.int32
+    for nd, ns in ((2, 0), (2, 3), (3, 0), (3, 5)):
+        img, lv = render(w, h, scene, d, levels=True, precision=prec, ndev=nd, nshards=ns)
+        assert np.array_equal(img.view(iv), one.view(iv)), (prec, nd, ns)
+        assert np.array_equal(lv, lv1), (prec, nd, ns)
+        pin = N.pinned_empty((h, w, 3), np.float64 if prec == "f64" else np.float32)
+        render(w, h, scene, d, precision=prec, ndev=nd, nshards=ns, out=pin)
+        assert np.array_equal(pin.view(iv), one.view(iv)), (prec, nd, ns, "pinned")
+s1 = render(96, 72, scenes.named("s256"), 8, spp=4)
+s3 = render(96, 72, scenes.named("s256"), 8, spp=4, ndev=3)
+assert np.array_equal(s1.view(np.int64), s3.view(np.int64))
+print("aliases ok")
+"""
+    env = dict(os.environ, RT_DEVICE_ALIAS="3", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "aliases ok" in r.stdout, r.stdout + r.stderr
+
+
 def test_distributed_strategy_all_devices():
     """raytraced_pixel_list_distributed/4 (every visible device) returns the concurrent list."""
     a = rt.raytraced_pixel_list_distributed(40, 30, records.scene(), 3)
