@@ -103,7 +103,9 @@ typedef struct rt_elem {
 typedef struct rt_opts {
     uint32_t struct_size; /* sizeof(rt_opts); 0 or a NULL opts pointer selects every default */
     int32_t first_dev;    /* first HIP device (default 0) */
-    int32_t ndev;         /* devices used by rt_render in this process (default 1; -1 = all visible) */
+    int32_t ndev;         /* devices used by rt_render in this process (default 1; -1 = all visible).
+                             Test hook: the environment variable RT_DEVICE_ALIAS=N (1..4, read once
+                             per process) makes rt_render see N devices that are all first_dev */
     int32_t precision;    /* RT_OUT_F64 (default) or RT_OUT_F32 */
     int32_t order;        /* RT_ORDER_EXACT (default) or RT_ORDER_FAST */
     uint32_t row_block;   /* multi-device interleave granularity in rows (default 16) */
