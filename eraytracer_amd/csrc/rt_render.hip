@@ -1256,6 +1256,9 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
             const unsigned long long *occ = occ_masks<SPH>(S, light, chunk >> 6);
             const int ncell = SPH == 2 ? 1 : h.occ_cells;
             unsigned long long mine = blocked ? 0ull : occ[(loc * ncell + cell) * h.n_chunk]; // never holds the target
+#ifdef RT_ABL_NO_OCC // timing ablation builds only (results wrong): no occluder tests
+            mine = 0;
+#endif
             for (;;) {
                 const bool w = !blocked && mine != 0;
                 if (__ballot(w) == 0) break;
