@@ -2264,6 +2264,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         }
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
+        const int sblocks1 = std::min<int>(STRIDE_BLOCKS_L1, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
         // level k's dense list, then its shading (k_light reads only level k: on a side stream
         // it starts as soon as the list exists and runs beside the next reflections)
         auto level_lists = [&](int k) -> int {
@@ -2342,7 +2343,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             KtScope kt(p, k == 1 ? RT_KT_LEVEL1 : 0, st);
             if (fuse) {
 #define RT_RS(SPHV, ILPV, LDSV, BVHV)                                                                               \
-    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV>), dim3(sblocks), dim3(BLOCK), LDSV, st, rhdr,   \
+    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV>), dim3(k == 1 ? sblocks1 : sblocks), dim3(BLOCK), \
+                       LDSV, st, rhdr,                                                                              \
                        p->d_tab, p->d_itab, k, o, qk(k - 1), sk(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
                        colk(k - 1), hk(k), krk(k), g)
                 // levels traversing the sphere BVH (unstaged scenes only): the BVH instantiations
