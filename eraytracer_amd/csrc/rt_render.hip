@@ -2265,6 +2265,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
         const int sblocks1 = std::min<int>(STRIDE_BLOCKS_L1, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
+        const int sblocksw = std::min<int>(STRIDE_BLOCKS_WALK, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
         // level k's dense list, then its shading (k_light reads only level k: on a side stream
         // it starts as soon as the list exists and runs beside the next reflections)
         auto level_lists = [&](int k) -> int {
@@ -2386,7 +2387,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             // (fuse) the shadow answers are in the children's records (PAD)
             auto walk = [&](hipStream_t s_, int lo, int hi, bool deep) {
 #define RT_WALK_K(SPHV, BITSV, DEEPV, PADV, LDSV)                                                                    \
-    hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV, DEEPV, PADV>), dim3(sblocks), dim3(BLOCK), LDSV, s_,       \
+    hipLaunchKernelGGL((k_walk<PREC, GENPOW, SPHV, BITSV, DEEPV, PADV>), dim3(sblocksw), dim3(BLOCK), LDSV, s_,      \
                        p->hdr, p->d_tab, p->d_itab, D, o, q, ls_, lists, nitems, p->d_colbuf, p->d_child,            \
                        p->d_lit, lo, hi, g)
 #define RT_WALK(SPHV, BITSV, LDSV)                                                                                  \
