@@ -101,9 +101,11 @@ def self_launch(argv, nproc: int, run=subprocess.run) -> int:
 
 def cpu_baseline(scene, W, H, depth, target_s, spp=1, seed=0):
     """The C oracle in the reference's literal recursion (lighting_function recomputes the
-    reflection per light, raytracer.erl:211-224), threaded over the box's CPU share, on a
-    bounded sample of rows spread over the same frame.  The literal recursion is exponential
-    in depth (L^(depth-1) re-evaluations), so deeper or supersampled configs use the
+    reflection per light, raytracer.erl:211-224), threaded over the box's CPU share like the
+    `concurrent` strategy's workers (raytracer.erl:101-119), on a bounded sample of rows spread
+    over the same frame.  Every call renders a list of rows on all threads (orc_render_rows) and
+    `cores` is the number of threads that actually rendered rows.  The literal recursion is
+    exponential in depth (L^(depth-1) re-evaluations), so deeper or supersampled configs use the
     memoised oracle (same results) and say so."""
     from eraytracer_amd import _native as N
     from oracle import oracle as O
@@ -112,24 +114,28 @@ def cpu_baseline(scene, W, H, depth, target_s, spp=1, seed=0):
     threads = O.host_threads()  # this process's CPU share (OMP_NUM_THREADS, else its CPU affinity)
     literal = spp == 1 and depth <= 5
     mode = O.LITERAL if literal else O.MEMO
-    # calibrate on one row, then take evenly spaced rows to fill ~target_s seconds
+
+    def spread(n):
+        return sorted(set(int(r) for r in [(i * H) // n + (H // n) // 2 for i in range(n)]))
+
+    # calibrate on 2 rows per thread spread over the frame, then fill ~target_s seconds
+    cal = spread(min(H, 2 * threads))
     t0 = time.perf_counter()
-    O.render(el, W, H, depth, mode=mode, threads=threads, row0=H // 2, nrows=1, spp=spp, seed=seed)
-    per_row = max(time.perf_counter() - t0, 1e-4)
-    nrows = int(max(1, min(H, target_s / per_row)))
-    rows = sorted(set(int(r) for r in [(i * H) // nrows + (H // nrows) // 2 for i in range(nrows)]))
+    O.render_rows(el, W, H, cal, depth, mode=mode, threads=threads, spp=spp, seed=seed)
+    per_row = max(time.perf_counter() - t0, 1e-4) / len(cal)
+    rows = spread(int(max(threads, min(H, target_s / per_row))))
     t0 = time.perf_counter()
-    for r in rows:
-        O.render(el, W, H, depth, mode=mode, threads=threads, row0=r, nrows=1, spp=spp, seed=seed)
+    _, workers = O.render_rows(el, W, H, rows, depth, mode=mode, threads=threads, spp=spp, seed=seed)
     dt = time.perf_counter() - t0
     px = len(rows) * W
     how = ("ORC_LITERAL (the reference's per-light reflection recursion)" if literal else
            "ORC_MEMO (reflection once per hit; the literal recursion is exponential in depth)")
-    return {"value": px / dt / 1e6, "unit": "Mpixels/s", "cores": threads, "kind": "port",
+    return {"value": px / dt / 1e6, "unit": "Mpixels/s", "cores": workers, "kind": "port",
             "sample": f"{len(rows)} evenly spaced rows x {W} px of the same {W}x{H} depth-{depth}"
-                      + (f" x{spp} spp" if spp > 1 else "") + f" frame ({px} px, {dt:.1f} s), oracle/rt_oracle.c "
-                      f"{how}, {threads} threads; BEAM (erl) is not installed on the box",
-            "host": host_cpu_info()}
+                      + (f" x{spp} spp" if spp > 1 else "") + f" frame ({px} px, {dt:.1f} s) in one call, "
+                      f"oracle/rt_oracle.c {how}, {workers} of {threads} threads rendering rows; "
+                      "BEAM (erl) is not installed on the box",
+            "threads_requested": threads, "host": host_cpu_info()}
 
 
 def host_cpu_info():

@@ -93,38 +93,6 @@ __device__ __forceinline__ double sqrt_n(double x) {
     return __builtin_fma(d, h, g);
 }
 
-// 1 / sqrt(x) as normalize/1 computes it (:554-560): Mag = sqrt(x) rounded, then 1/Mag rounded —
-// the same two correctly rounded results as sqrt_n and div_n(1, .), but the reciprocal starts from
-// the square root's own half-reciprocal h (2h = 1/sqrt(x) to ~2^-46 after sqrt_n's Goldschmidt
-// step) instead of a fresh v_rcp_f64 and two Newton steps: one Newton step makes it faithful, and
-// the final correction step (div_n's last) rounds it correctly.  For x in [SQRT_N_LO, SQRT_N_HI]
-// with sqrt(x) in [RCP_N_LO, RCP_N_HI]; rt_selftest_math checks it bit for bit against the
-// library's sqrt and division.
-// Off: bit-identical to the library on 1.3e10 random operands (rt_selftest_math), yet the default
-// scene's frames differed from the oracle in 2.5 % of their pixels (<= 1.3e-14): some structured
-// operands (integer scene coordinates) round differently.  Kept for study.
-#ifndef RT_RCP_FROM_SQRT
-#define RT_RCP_FROM_SQRT 0
-#endif
-__device__ __forceinline__ double rsqrt_n(double x) {
-    const double s = __builtin_amdgcn_rsq(x);
-    double g = x * s;
-    double h = s * 0.5;
-    const double r = __builtin_fma(-h, g, 0.5);
-    g = __builtin_fma(g, r, g);
-    h = __builtin_fma(h, r, h);
-    double d = __builtin_fma(-g, g, x);
-    g = __builtin_fma(d, h, g);
-    d = __builtin_fma(-g, g, x);
-    const double m = __builtin_fma(d, h, g); // == sqrt_n(x)
-    double y = h + h;                        // exact
-    const double e = __builtin_fma(-m, y, 1.0);
-    y = __builtin_fma(y, e, y);
-    const double q = 1.0 * y;
-    const double rr = __builtin_fma(-m, q, 1.0);
-    return __builtin_fma(rr, y, q);
-}
-
 // a / b for |b| in [RCP_N_LO, RCP_N_HI] and |a| small enough that a/b is a normal number or 0
 __device__ __forceinline__ double div_n(double a, double b) {
     double y = __builtin_amdgcn_rcp(b);
@@ -179,7 +147,7 @@ __device__ __forceinline__ double sqrt_x(double x) { // == sqrt(x)
 __device__ __forceinline__ D3 normalize3(const D3 &v, bool fast = false) { // vector_normalize/1 (:554-560)
     const double m2 = v.x * v.x + v.y * v.y + v.z * v.z;
     if (fast || __ballot(!(m2 >= RCP_N_LO && m2 <= RCP_N_HI)) == 0) { // mag and 1/mag in range, mag != 0
-        const double s = RT_RCP_FROM_SQRT ? rsqrt_n(m2) : div_n(1.0, sqrt_n(m2));
+        const double s = div_n(1.0, sqrt_n(m2));
         return D3{v.x * s, v.y * s, v.z * s};
     }
     double mag = sqrt(m2);
@@ -1540,10 +1508,6 @@ __global__ __launch_bounds__(256) void k_selftest_math(unsigned long long n, uns
         const long long e = 1023 - 767 + (long long)((r >> 52) % (767 + 1000));
         const double x = __longlong_as_double((long long)((unsigned long long)e << 52 | (r & 0xFFFFFFFFFFFFFull)));
         if (__double_as_longlong(sqrt_n(x)) != __double_as_longlong(sqrt(x))) ++local;
-        // 1 / sqrt(y) over normalize3's fast range [2^-400, 2^400] (Mag and its reciprocal in range)
-        const long long ey = 1023 - 400 + (long long)((r >> 52) % 800);
-        const double yv = __longlong_as_double((long long)((unsigned long long)ey << 52 | (r & 0xFFFFFFFFFFFFFull)));
-        if (RT_RCP_FROM_SQRT && __double_as_longlong(rsqrt_n(yv)) != __double_as_longlong(1.0 / sqrt(yv))) ++local;
         // structured operands (scenes are written with small integers and short fractions): the
         // squared length of a vector of integers in [-2^10, 2^10] scaled by 2^-k
         {
@@ -1601,10 +1565,8 @@ struct rt_prepared {
     size_t colbuf_bytes = 0;
     int *d_counts = nullptr;  // per level and tile: queue lengths
     size_t counts_bytes = 0;
-    int *d_items = nullptr;   // per-level record counts and sort histograms, then per-level dense slot lists
+    int *d_items = nullptr;   // per-level record counts, then per-level dense slot lists
     size_t items_bytes = 0;
-    int2 *d_keyrank = nullptr; // sorted levels: per level and slot, the record's (bin, rank in the bin)
-    size_t keyrank_bytes = 0;
     // primary rays' candidate masks per 8x16 pixel block of the slab (k_pmask), kept while the
     // frame geometry and the scene stay the same
     unsigned long long *d_pmask = nullptr;
@@ -1939,7 +1901,6 @@ int rt_release(rt_prepared *p) {
     if (p->d_sample) (void)hipFree(p->d_sample);
     if (p->d_counts) (void)hipFree(p->d_counts);
     if (p->d_items) (void)hipFree(p->d_items);
-    if (p->d_keyrank) (void)hipFree(p->d_keyrank);
     if (p->d_pmask) (void)hipFree(p->d_pmask);
     for (hipEvent_t &e : p->ev_level)
         if (e) (void)hipEventDestroy(e);
@@ -1977,7 +1938,6 @@ size_t rt_trim(rt_prepared *p) {
     drop(reinterpret_cast<void *&>(p->d_sample), p->sample_bytes);
     drop(reinterpret_cast<void *&>(p->d_counts), p->counts_bytes);
     drop(reinterpret_cast<void *&>(p->d_items), p->items_bytes);
-    drop(reinterpret_cast<void *&>(p->d_keyrank), p->keyrank_bytes);
     drop(reinterpret_cast<void *&>(p->d_pmask), p->pmask_bytes);
     p->pmask_valid = false;
     ++p->gen; // captured frame graphs hold the old pointers
@@ -2031,49 +1991,6 @@ int grow(void **buf, size_t *have, size_t need, unsigned *gen) {
     return RT_OK;
 }
 
-// Primary rays' candidate masks precomputed per frame geometry (k_pmask); RT_PMASK=0 builds the
-// beams in k_primary every frame, for A/B runs.
-bool pmask_on() {
-    static const bool on = [] {
-        const char *e = std::getenv("RT_PMASK");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    return on;
-}
-
-// Each level's shading fused into the next reflection pass (k_reflect_shade) when the context runs
-// without side streams; RT_FUSE_SHADE=0 keeps separate k_light launches, for A/B runs.
-bool fuse_on() {
-    static const bool on = [] {
-        const char *e = std::getenv("RT_FUSE_SHADE");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    return on;
-}
-
-// Sorted deep levels (SORT_BINS): RT_SORT=0 off (default), 1 scenes with the sphere BVH (many
-// spheres: incoherent deep levels), 2 every spheres-only scene — for A/B runs.  Measured round 4
-// (config 5, kernels alone per sample pass): the BVH levels 2-7 got 7 % faster (1,135 -> 1,067 us)
-// but the sorted lists' scattered writes made k_items 6x slower (+320 us) and the producer's keys
-// cost +30 us — config 5 32.0 -> 32.4 ms per frame; config 3 (RT_SORT=2) -2 %.  Not on by default.
-int sort_mode() {
-    static const int m = [] {
-        const char *e = std::getenv("RT_SORT");
-        return e ? std::atoi(e) : 0;
-    }();
-    return m;
-}
-
-// RT_MISS_MEMSET=1: spp = 1 passes zero their image rows with a fill before k_primary, which then
-// skips the misses' pixels (A/B).
-bool miss_memset_on() {
-    static const bool on = [] {
-        const char *e = std::getenv("RT_MISS_MEMSET");
-        return e && std::strcmp(e, "1") == 0;
-    }();
-    return on;
-}
-
 // The slab rows of shard sh that lie inside the image (a prefix of the slab).
 size_t valid_slab_rows(int H, int rb, int sh, int ns) {
     const size_t slab = rt_shard_rows((uint32_t)H, (uint32_t)rb, (uint32_t)ns);
@@ -2091,7 +2008,7 @@ size_t valid_slab_rows(int H, int rb, int sh, int ns) {
 bool wave_single_write(const rt_prepared *p, int D, bool levels) {
     const int nrefl = (p->hdr.n_light > 0 && D > 1) ? D - 1 : 0;
     const bool overlap = lit_overlap(p) && D > 1 && p->hdr.n_light > 0;
-    return nrefl == 0 || (fuse_on() && !overlap && !levels);
+    return nrefl == 0 || (!overlap && !levels);
 }
 
 // acc (slab row 0, binary64, or null): supersampled passes fold their sample into it where each
@@ -2126,24 +2043,17 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_counts), &p->counts_bytes, max_tiles * nlev * sizeof(int), &p->gen);
     const bool overlap = lit_overlap(p) && D > 1 && p->hdr.n_light > 0;
-    // levels 1 .. nrefl - 1 (each shaded and reflected by k_reflect_shade) listed in sort-key order
-    const int nrefl_ = (p->hdr.n_light > 0 && D > 1) ? D - 1 : 0;
-    const bool sorted = fuse_on() && !overlap && !levels && nrefl_ > 1 && p->hdr.n_tri == 0 && p->hdr.n_pl == 0 &&
-                        p->hdr.cull_ok && (sort_mode() == 2 || (sort_mode() == 1 && p->hdr.bvh_ok));
-    // dense work lists: 64 per-level record counts, per level the sort histogram, then per level the
-    // slots of its records in tile order, then (sorted) in sort-key order
-    const size_t list0 = 64 + (size_t)nlev * SORT_BINS;
-    const size_t items_ints = list0 + slots * nlev * (sorted ? 2 : 1);
+    // dense work lists: 64 per-level record counts, then per level the slots of its records in tile order
+    const size_t list0 = 64;
+    const size_t items_ints = list0 + slots * nlev;
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_items), &p->items_bytes, items_ints * sizeof(int), &p->gen);
-    if (rc == RT_OK && sorted)
-        rc = grow(reinterpret_cast<void **>(&p->d_keyrank), &p->keyrank_bytes, slots * nlev * sizeof(int2), &p->gen);
     if (rc == RT_OK && overlap) rc = side_stream(p);
     if (rc != RT_OK) return rc;
     // the primary rays' candidate masks of the whole slab (k_pmask), recomputed only when the
     // frame geometry or the scene changed (or after rt_trim)
     const unsigned long long *pmask = nullptr;
-    if (p->hdr.beam_ok && D > 0 && pmask_on()) {
+    if (p->hdr.beam_ok && D > 0) {
         const int slab_all = (int)rt_shard_rows(H, rb, ns);
         const size_t nhalf = (size_t)tiles_x * ((slab_all + TILE - 1) / TILE) * 2;
         const long long key[8] = {W, H, rb, sh, ns, spp > 1, (long long)p->scene_gen, slab_all};
@@ -2175,46 +2085,30 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     const int nrefl = (p->hdr.n_light > 0 && D > 1) ? D - 1 : 0;
     const int nshade = D > 0 ? 1 + nrefl : 0;
     // spheres only, culling on: every shadow target has occluder masks (lit_by<1>); their
-    // per-lane-gathered tables staged in each workgroup's LDS when they fit (SPH = 2;
-    // RT_LDS_STAGE=0 keeps them in HBM, for A/B runs)
+    // per-lane-gathered tables staged in each workgroup's LDS when they fit (SPH = 2)
     const bool sph_only = p->hdr.n_tri == 0 && p->hdr.n_pl == 0 && p->hdr.cull_ok;
-    static const bool stage_env = [] {
-        const char *e = std::getenv("RT_LDS_STAGE");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    const bool staged = sph_only && stage_env && p->hdr.l_bytes > 0;
+    const bool staged = sph_only && p->hdr.l_bytes > 0;
     const size_t lds = staged ? (size_t)p->hdr.l_bytes : 0;
     // Reflection kernels of levels that traverse the sphere BVH: after the staged tables in LDS,
     // the BVH nodes and sphere rows (when they fit BVH_LDS_MAX) and every lane's stack.
     SceneHdr rhdr = p->hdr;
     size_t lds_bvh = lds;
     if (rhdr.bvh_ok) {
-        // RT_BVH_ROWS_LDS=0: the sphere rows stay in HBM (L1/L2 hits), leaving LDS to the nodes and
-        // a deeper stack (A/B)
-        static const bool rows_lds = [] {
-            const char *e = std::getenv("RT_BVH_ROWS_LDS");
-            return !(e && std::strcmp(e, "0") == 0);
-        }();
-        const size_t nb = (size_t)rhdr.n_bvh * BVH_NODE_DOUBLES * 8, sb = rows_lds ? (size_t)rhdr.n_sph * SPH_W * 8 : 0;
+        const size_t nb = (size_t)rhdr.n_bvh * BVH_NODE_DOUBLES * 8, sb = (size_t)rhdr.n_sph * SPH_W * 8;
         if (nb + sb <= (size_t)BVH_LDS_MAX) {
             rhdr.l_bvh = (int)lds_bvh;
-            rhdr.l_bsph = rows_lds ? (int)(lds_bvh + nb) : -1;
+            rhdr.l_bsph = (int)(lds_bvh + nb);
             lds_bvh += nb + sb;
         }
         rhdr.l_stack = (int)lds_bvh;
         lds_bvh += (size_t)BLOCK * rhdr.bvh_depth * sizeof(unsigned);
     }
-    // RT_BVH_STAGED=1 (A/B; with RT_BVH_MIN below the scene's sphere count): the BVH levels of an
-    // LDS-staged scene traverse it too, its nodes, rows and stacks placed after the staged tables
-    static const bool bvh_staged = [] {
-        const char *e = std::getenv("RT_BVH_STAGED");
-        return e && std::strcmp(e, "1") == 0;
-    }();
-    auto bvh_at = [&](int k) { return (!staged || bvh_staged) && rhdr.bvh_ok && k >= rhdr.bvh_level; };
+    // (LDS-staged scenes keep the candidate walks: their tables and the BVH would not fit together)
+    auto bvh_at = [&](int k) { return !staged && rhdr.bvh_ok && k >= rhdr.bvh_level; };
     auto lds_r = [&](int k) { return bvh_at(k) ? lds_bvh : lds; };
     // no side streams (frames in flight): each level's shading fused into the next reflection
     // pass (k_reflect_shade)
-    const bool fuse = fuse_on() && !overlap && !levels && nrefl > 0;
+    const bool fuse = !overlap && !levels && nrefl > 0;
     for (int row0 = row_begin; row0 < row_end; row0 += pass_rows) {
         const int rows = std::min(pass_rows, row_end - row0);
         const int ntiles = tiles_x * ((rows + TILE - 1) / TILE);
@@ -2230,37 +2124,23 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         int *nitems = p->d_items; // [0, 64): per-level record counts
         int *lists = p->d_items + list0;
         auto ik = [&](int k) { return lists + (size_t)k * ntiles * TILE_SLOTS; };
-        auto is_sorted = [&](int k) { return sorted && k >= 1 && k < nrefl; };
-        auto hk = [&](int k) { return is_sorted(k) ? p->d_items + 64 + (size_t)k * SORT_BINS : nullptr; };
-        auto krk = [&](int k) { return is_sorted(k) ? p->d_keyrank + (size_t)k * ntiles * TILE_SLOTS : nullptr; };
-        auto sk = [&](int k) { return is_sorted(k) ? lists + (size_t)(nlev + k) * ntiles * TILE_SLOTS : ik(k); };
         auto colk = [&](int k) { return k > 0 ? p->d_colbuf + (size_t)(k - 1) * ntiles * TILE_SLOTS * COL_W : nullptr; };
         auto chk = [&](int k) { return p->d_child + (size_t)k * ntiles * TILE_SLOTS; };
         auto litk = [&](int k) { return p->d_lit + (size_t)k * ntiles * TILE_SLOTS; };
-        HIPCHK(hipMemsetAsync(nitems, 0, (sorted ? list0 : 64) * sizeof(int), st));
+        HIPCHK(hipMemsetAsync(nitems, 0, list0 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
         const PassGeom g{W, H, rb, sh, ns, row0, spp, sample, seed, acc_p}; // level-0 records are rebuilt from it
         const dim3 grid(std::min(ntiles, PRIMARY_GRID)); // k_primary: grid-stride loop over the tiles
         {
             KtScope kt(p, RT_KT_PRIMARY, st);
-            // RT_MISS_MEMSET=1 (A/B): the pass's image rows zeroed by a fill (streamed full lines),
-            // k_primary then writes only hits' records, not the misses' scattered 12-byte pixels
-            int preset = 0;
-            if (miss_memset_on() && acc_p == nullptr) {
-                const int valid = (int)std::min<size_t>((size_t)rows, valid_slab_rows(H, rb, sh, ns) > (size_t)row0
-                                                                           ? valid_slab_rows(H, rb, sh, ns) - row0 : 0);
-                if (valid > 0)
-                    HIPCHK(hipMemsetAsync(o, 0, (size_t)valid * W * 3 * (PREC == RT_OUT_F64 ? 8 : 4), st));
-                preset = 1;
-            }
             if (lv0)
                 hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W,
                                    H, D, rb, sh, ns, rows, row0, o, lv0, q, p->d_counts, ntiles, spp, sample, seed, acc_p,
-                                   pmask, preset);
+                                   pmask);
             else
                 hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
                                    W, H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed, acc_p,
-                                   pmask, preset);
+                                   pmask);
         }
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
@@ -2269,49 +2149,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         // level k's dense list, then its shading (k_light reads only level k: on a side stream
         // it starts as soon as the list exists and runs beside the next reflections)
         auto level_lists = [&](int k) -> int {
-            hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k, hk(k), krk(k),
-                               sk(k));
+            hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k);
             HIPCHK(hipGetLastError());
-#ifdef RT_DEBUG_LISTS
-            if (is_sorted(k)) {
-                HIPCHK(hipStreamSynchronize(st));
-                int n = 0;
-                HIPCHK(hipMemcpy(&n, nitems + k, 4, hipMemcpyDeviceToHost));
-                std::vector<int> a(n), b(n), hh(SORT_BINS);
-                std::vector<int2> kr((size_t)ntiles * TILE_SLOTS);
-                HIPCHK(hipMemcpy(a.data(), ik(k), 4 * (size_t)n, hipMemcpyDeviceToHost));
-                HIPCHK(hipMemcpy(b.data(), sk(k), 4 * (size_t)n, hipMemcpyDeviceToHost));
-                HIPCHK(hipMemcpy(hh.data(), hk(k), 4 * SORT_BINS, hipMemcpyDeviceToHost));
-                HIPCHK(hipMemcpy(kr.data(), krk(k), 8 * kr.size(), hipMemcpyDeviceToHost));
-                long long hs = 0;
-                for (int x : hh) hs += x;
-                std::vector<int> sa = a, sb = b;
-                std::sort(sa.begin(), sa.end());
-                std::sort(sb.begin(), sb.end());
-                {
-                    std::vector<int> cn(ntiles);
-                    HIPCHK(hipMemcpy(cn.data(), ck(k), 4 * (size_t)ntiles, hipMemcpyDeviceToHost));
-                    std::vector<HitRec> rec((size_t)ntiles * TILE_SLOTS);
-                    HIPCHK(hipMemcpy(rec.data(), qk(k), sizeof(HitRec) * rec.size(), hipMemcpyDeviceToHost));
-                    std::vector<int> seen(SORT_BINS * 64, 0);
-                    for (int x : a) {
-                        const int2 v = kr[x];
-                        const bool okk = v.x >= 0 && v.x < SORT_BINS && v.y >= 0 && v.y < hh[v.x];
-                        if (!okk || (v.y < 64 && seen[v.x * 64 + v.y]++))
-                            std::fprintf(stderr, "  level %d slot %d (tile %d cnt %d): key %d rank %d bin %d; rec pix %d obj %d parent %d\n",
-                                         k, x, x >> 8, cn[x >> 8], v.x, v.y, okk ? hh[v.x] : -1, rec[x].pix, rec[x].obj,
-                                         rec[x].parent);
-                    }
-                }
-                if (sa != sb || hs != n) {
-                    std::fprintf(stderr, "RT_DEBUG_LISTS sample %d level %d: n %d hist %lld, lists differ\n", sample, k, n, hs);
-                    for (int x : a) {
-                        if (!std::binary_search(sb.begin(), sb.end(), x))
-                            std::fprintf(stderr, "  missing slot %d key %d rank %d (bin count %d)\n", x, kr[x].x, kr[x].y, hh[kr[x].x & (SORT_BINS - 1)]);
-                    }
-                }
-            }
-#endif
             if (overlap) {
                 HIPCHK(hipEventRecord(p->ev_level[k], st));
                 HIPCHK(hipStreamWaitEvent(ls(k), p->ev_level[k], 0));
@@ -2346,8 +2185,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
 #define RT_RS(SPHV, ILPV, LDSV, BVHV)                                                                               \
     hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV>), dim3(k == 1 ? sblocks1 : sblocks), dim3(BLOCK), \
                        LDSV, st, rhdr,                                                                              \
-                       p->d_tab, p->d_itab, k, o, qk(k - 1), sk(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
-                       colk(k - 1), hk(k), krk(k), g)
+                       p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
+                       colk(k - 1), g)
                 // levels traversing the sphere BVH (unstaged scenes only): the BVH instantiations
                 const bool bvh_k = bvh_at(k);
                 if (staged && bvh_k) RT_RS(2, true, lds_r(k), true);
@@ -2511,7 +2350,7 @@ int launch_frame(rt_prepared *p, const long long (&args)[12], hipStream_t st, F 
 // (default scene 1920x1080 d5: 15.1 vs 6.1 Gpx/s); larger ones by the scans, where the wavefront
 // pipeline's coherent waves and overlap win (round 1, 4096^2 d5: wavefront ahead from 48
 // objects), and spheres-only scenes with LDS-staged tables at any size (below).
-// RT_ENGINE=fused | wave forces one; RT_FUSED_MAX_OBJECTS moves the crossover.
+// RT_ENGINE=fused | wave forces one.
 constexpr int FUSED_MAX_OBJECTS = 40;
 bool use_mega_engine(const rt_prepared *p) {
     static const int mode = [] { // 0 auto, 1 fused, 2 wave
@@ -2520,10 +2359,6 @@ bool use_mega_engine(const rt_prepared *p) {
         if (s && std::strcmp(s, "wave") == 0) return 2;
         return 0;
     }();
-    static const int max_obj = [] {
-        const char *s = std::getenv("RT_FUSED_MAX_OBJECTS");
-        return s ? std::atoi(s) : FUSED_MAX_OBJECTS;
-    }();
     if (mode) return mode == 1;
     // spheres-only scenes whose tables are staged in LDS: the wavefront engine at every size
     // (measured round 2, 4096^2 d5, 4 frames in flight: S4 115 vs 89 Gpx/s, S8 86 vs 70,
@@ -2531,7 +2366,7 @@ bool use_mega_engine(const rt_prepared *p) {
     // RT_CFG_CULL = 0 strips, so the brute-force mode runs the production engine.
     const SceneHdr &h = p->hdr_full;
     if (h.n_tri == 0 && h.n_pl == 0 && h.cull_ok && h.l_bytes > 0) return false;
-    return h.n_obj <= max_obj;
+    return h.n_obj <= FUSED_MAX_OBJECTS;
 }
 
 } // namespace
@@ -2585,11 +2420,7 @@ int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dep
     const int r0 = (int)row_begin, r1 = (int)row_end, slab_rows = (int)slab;
     if (spp > 1) { // RT_SUPERSAMPLING, on the wavefront engine: one pass per sample, summed in order
         // the slab rows inside the image (a prefix: global rows grow with slab rows)
-        size_t valid_rows = 0;
-        for (int blk = 0; blk * rb < slab_rows; ++blk) {
-            const long long base = ((long long)blk * ns + sh) * rb;
-            valid_rows += (size_t)std::max(0LL, std::min((long long)rb, (long long)H - base));
-        }
+        const size_t valid_rows = valid_slab_rows(H, rb, sh, ns);
         const size_t v1 = std::min<size_t>(valid_rows, (size_t)r1);
         if (v1 <= (size_t)r0) return RT_OK;
         const size_t e0 = (size_t)r0 * W * 3, n = (v1 - r0) * W * 3; // the band's elements

@@ -147,12 +147,9 @@ static void build_bvh(const std::vector<rt_elem> &e, const std::vector<int> &sph
     while ((1 << depth) < n) ++depth;
     if (depth > BVH_STACK) return; // a node at depth i holds at most i stack entries, pushes one more
     // Surface-area-heuristic splits among those that keep every leaf within ceil(log2 n) + slack
-    // levels (the traversal stack's size; BVH_SAH_SLACK, RT_BVH_SAH_SLACK; 0: median splits).
-    // Measured, config 5: slack 2 -2.2 % per frame against median splits.
-    static const int slack = [] {
-        const char *s = std::getenv("RT_BVH_SAH_SLACK");
-        return s ? std::atoi(s) : BVH_SAH_SLACK;
-    }();
+    // levels (the traversal stack's size; BVH_SAH_SLACK; 0: median splits).
+    // Measured, config 5: slack 2 -2.2 % per frame against median splits; 1 or 3 neutral.
+    constexpr int slack = BVH_SAH_SLACK;
     const int cap = slack > 0 && depth + 1 <= BVH_STACK ? std::min(depth + slack, BVH_STACK) : 0;
     double ext = 0;
     for (const rt_vec3 &o : org) ext = std::fmax(ext, std::fmax(std::fabs(o.x), std::fmax(std::fabs(o.y), std::fabs(o.z))));
@@ -333,13 +330,8 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
     // any-hit — so the spheres that cover most of the lights' view go first: a shadow ray's
     // occluder walk meets the likelier blockers early and its lane leaves sooner (measured against
     // list order: config 5 -4.5 % per frame, config 3 -1 %; ordering by radius alone: -3 %, and +1 %
-    // on config 3).  RT_SPH_ORDER=list keeps the list order, for A/B.
-    static const int order = [] {
-        const char *s = std::getenv("RT_SPH_ORDER");
-        return !s ? 0 : std::strcmp(s, "list") == 0 ? 1 : std::strcmp(s, "radius") == 0 ? 2 : 0;
-    }();
-    const bool by_radius = order != 1;
-    if (by_radius) {
+    // on config 3).
+    {
         // the spheres' solid angle summed over the lights (their radius when there are none)
         std::vector<double> w(e.size(), 0.0);
         for (int i : sph) {

@@ -42,6 +42,9 @@ def lib():
         L.orc_render_spp.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_render_rows.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_focal_length.restype = ctypes.c_double
         L.orc_focal_length.argtypes = [ctypes.c_double, ctypes.c_double]
         L.orc_vec_op.argtypes = [ctypes.c_int, dp, dp, ctypes.c_double, dp]
@@ -87,6 +90,21 @@ def render(elems, width, height, depth, mode=MEMO, threads=None, row0=0, nrows=N
     if rc != 0:
         raise ValueError(f"oracle render failed: {rc}")
     return (out, lv) if levels else out
+
+
+def render_rows(elems, width, height, rows, depth, mode=MEMO, threads=None, spp=1, seed=0):
+    """Render the listed image rows in one threaded call (the rows shared out over `threads`
+    threads through one counter).  Returns ((len(rows), width, 3) float64 array, the number of
+    threads that rendered at least one row)."""
+    if threads is None:
+        threads = host_threads()
+    rows = np.ascontiguousarray(np.asarray(rows, dtype=np.uint32))
+    out = np.zeros((len(rows), width, 3), dtype=np.float64)
+    rc = lib().orc_render_rows(ctypes.cast(elems, ctypes.c_void_p), len(elems), width, height, rows.ctypes.data,
+                               len(rows), depth, mode, threads, spp, seed, out.ctypes.data, None)
+    if rc < 1:
+        raise ValueError(f"oracle render_rows failed: {rc}")
+    return out, int(rc)
 
 
 OPS = {"add": 0, "sub": 1, "square_mag": 2, "mag": 3, "scalar_mult": 4, "component_mult": 5, "dot": 6,

@@ -362,6 +362,8 @@ typedef struct {
     volatile uint32_t *next;
     uint32_t spp;
     uint64_t seed;
+    const uint32_t *rows;      /* NULL: rows row0 .. row0+nrows-1; else the listed rows */
+    volatile uint32_t *workers; /* threads that rendered at least one row */
 } Job;
 
 /* RT_SUPERSAMPLING (include/rt_mi355x.h; not part of the reference): the jitter hash. */
@@ -374,10 +376,13 @@ static uint64_t splitmix64(uint64_t z) {
 
 static void *worker(void *arg) {
     Job *j = (Job *)arg;
+    int worked = 0;
     for (;;) {
         uint32_t r = __sync_fetch_and_add(j->next, 1);
         if (r >= j->nrows) break;
-        uint32_t y = j->row0 + r;
+        if (!worked && j->workers) __sync_fetch_and_add(j->workers, 1);
+        worked = 1;
+        uint32_t y = j->rows ? j->rows[r] : j->row0 + r;
         for (uint32_t x = 0; x < j->W; x++) {
             int lv = 0;
             V c;
@@ -411,6 +416,15 @@ static void *worker(void *arg) {
     return NULL;
 }
 
+static void run_job(Job *job, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    for (int t = 1; t < threads; t++) pthread_create(&tid[t], NULL, worker, job);
+    worker(job);
+    for (int t = 1; t < threads; t++) pthread_join(tid[t], NULL);
+}
+
 /* Render rows [row0, row0+nrows) of a W x H image into out (nrows*W*3 doubles), spp
  * samples per pixel (RT_SUPERSAMPLING; spp = 1 is the reference's pixel loop). */
 int orc_render_spp(const rt_elem *scene, uint32_t n, uint32_t W, uint32_t H, uint32_t row0, uint32_t nrows,
@@ -420,14 +434,26 @@ int orc_render_spp(const rt_elem *scene, uint32_t n, uint32_t W, uint32_t H, uin
     if (row0 + nrows > H) return RT_EBADARG;
     Scene sc = {scene, n};
     volatile uint32_t next = 0;
-    Job job = {&sc, W, H, row0, nrows, depth, mode, out, levels, &next, spp ? spp : 1, seed};
-    if (threads < 1) threads = 1;
-    if (threads > 256) threads = 256;
-    pthread_t tid[256];
-    for (int t = 1; t < threads; t++) pthread_create(&tid[t], NULL, worker, &job);
-    worker(&job);
-    for (int t = 1; t < threads; t++) pthread_join(tid[t], NULL);
+    Job job = {&sc, W, H, row0, nrows, depth, mode, out, levels, &next, spp ? spp : 1, seed, NULL, NULL};
+    run_job(&job, threads);
     return RT_OK;
+}
+
+/* Render the listed rows rows[0..nrows) of a W x H image (out row i = image row rows[i]) on
+ * `threads` threads, the rows shared out through one counter as in the `concurrent` strategy's
+ * workers (raytracer.erl:101-119).  Returns the number of threads that rendered at least one
+ * row (>= 1), or a negative RT_E* code. */
+int orc_render_rows(const rt_elem *scene, uint32_t n, uint32_t W, uint32_t H, const uint32_t *rows, uint32_t nrows,
+                    int depth, int mode, int threads, uint32_t spp, uint64_t seed, double *out, uint8_t *levels) {
+    if (n < 1 || scene[0].kind != RT_CAMERA) return RT_EBADARG;
+    if (W == 0 || H == 0 || rows == NULL || nrows == 0) return RT_EBADARG;
+    for (uint32_t i = 0; i < nrows; i++)
+        if (rows[i] >= H) return RT_EBADARG;
+    Scene sc = {scene, n};
+    volatile uint32_t next = 0, workers = 0;
+    Job job = {&sc, W, H, 0, nrows, depth, mode, out, levels, &next, spp ? spp : 1, seed, rows, &workers};
+    run_job(&job, threads);
+    return (int)workers;
 }
 
 int orc_render(const rt_elem *scene, uint32_t n, uint32_t W, uint32_t H, uint32_t row0, uint32_t nrows,

@@ -274,3 +274,34 @@ def test_term_types_rule(oracle, mk, d):
             assert kinds == {int} and rgb == (0, 0, 0), (i, rgb)
         else:
             assert kinds == {float}, (i, rgb)
+
+
+def test_render_rows_uses_every_thread(oracle):
+    """bench.py's cpu_baseline renders its row sample in one orc_render_rows call: the listed rows
+    equal the same rows of a whole-frame render bit for bit, every requested thread renders rows
+    (the returned worker count), and N threads run >= 0.7 N x faster than one."""
+    import time
+    el = N.marshal(scenes.s64())
+    W, H, d = 192, 192, 5
+    rows = list(range(1, H, 2))
+    full = oracle.render(el, W, H, d, mode=oracle.LITERAL, threads=2)
+    out, workers = oracle.render_rows(el, W, H, rows, d, mode=oracle.LITERAL, threads=2)
+    assert np.array_equal(out, full[rows])
+    n = max(1, min(4, len(os.sched_getaffinity(0))))
+
+    oracle.render_rows(el, W, H, rows, d, mode=oracle.LITERAL, threads=n)  # warm (clocks, pages)
+
+    def timed(t):
+        best = None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            _, w = oracle.render_rows(el, W, H, rows, d, mode=oracle.LITERAL, threads=t)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        return best, w
+
+    t1, w1 = timed(1)
+    tn, wn = timed(n)
+    assert w1 == 1 and wn == n
+    if n > 1:
+        assert t1 / tn >= 0.7 * n, (t1, tn, n)
