@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--no-boundary", action="store_true")
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight per rank (default 4 at N=1, 3 at N>1; 1 for --gather dense)")
+    ap.add_argument("--priorities", default="auto",
+                    help="comma-separated stream priority per in-flight slot (torch: lower = higher priority; "
+                         "auto: FrameRenderer's default, half the slots high with >= 4 in flight and spp 1; none)")
     ap.add_argument("--gather", default="compact", choices=["compact", "dense"],
                     help="N > 1: compact = background pixels not sent (rt_slab_pack, default); dense = whole slabs")
     return ap.parse_args()
@@ -227,7 +230,9 @@ def main():
     counts = workload.scene_counts(scene)
     inflight = args.inflight or (1 if args.gather == "dense" and world > 1 else 4 if world == 1 else 3)
     fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
-                       precision=args.precision, order=args.order, spp=args.spp, seed=args.seed, inflight=inflight)
+                       precision=args.precision, order=args.order, spp=args.spp, seed=args.seed, inflight=inflight,
+                       priorities=("auto" if args.priorities == "auto" else None if args.priorities == "none" else
+                                   [int(x) for x in args.priorities.split(",")]))
 
     # untimed: work count of this rank's rows (levels of every pixel's reflection chain)
     lv_fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
@@ -421,6 +426,7 @@ def main():
                        "width": W, "height": H, "depth": args.depth, "order": args.order,
                        "framebuffer": args.precision, "row_block": args.row_block, "inflight": inflight,
                        "engine": engine,
+                       "stream_priorities": [st.priority for st in fr.streams] if fr.streams else None,
                        "parallelism": f"rows{world}" + (f"+rccl_{args.gather}_gather" if world > 1 else ""),
                        "world_size": world, "rccl_ranks": dist.get_world_size() if world > 1 else 1,
                        "spheres": counts["spheres"], "triangles": counts["triangles"], "planes": counts["planes"],

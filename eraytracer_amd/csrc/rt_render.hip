@@ -110,16 +110,24 @@ __device__ __forceinline__ double div_n(double a, double b) {
 // shift (one v_ldexp_f64 instead of v_rcp_f64 and seven fma / mul) — the same bits.  n (uniform)
 // is made opaque where it is used: otherwise the compiler hoists (double) n and its reciprocal out
 // of the kernels' record loops into VGPRs that stay live (and spilled) across everything.
+// A wave-uniform value made opaque where it is used: a test on it (and what the compiler derives from
+// it) is evaluated there, in a few SALU instructions, instead of being hoisted out of the record loops
+// as a 64-bit condition mask held in SGPRs — which spilled to VGPR lanes (v_writelane / v_readlane).
+template <typename T>
+__device__ __forceinline__ T opq(T v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
 __device__ __forceinline__ double div_dim(double a, int n) {
+    n = opq(n);
     if ((n & (n - 1)) == 0) return __builtin_amdgcn_ldexp(a, -__builtin_ctz((unsigned)n)); // (wave-uniform)
-    asm volatile("" : "+s"(n));
     return div_n(a, (double)n);
 }
 // floor(a / n) for 0 <= a < 2^31, 1 <= n <= 2^20: a shift for a power of two; otherwise the
 // correctly rounded binary64 quotient, which truncates to the exact integer quotient
 __device__ __forceinline__ int idiv_dim(int a, int n) {
+    n = opq(n);
     if ((n & (n - 1)) == 0) return a >> __builtin_ctz((unsigned)n); // (wave-uniform)
-    asm volatile("" : "+s"(n));
     return (int)div_n((double)a, (double)n);
 }
 // The lane's index in its wave, opaque to the optimiser: lane masks derived from it are recomputed
