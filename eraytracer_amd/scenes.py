@@ -135,7 +135,9 @@ def synthetic_mixed(n_spheres: int = 48, seed: int = 0x5EED0048, powers=(1, 4, 2
 def named(name: str):
     from .records import scene as default_scene
     table = {"default": default_scene, "s64": s64, "s256": s256, "default_powers": default_powers,
-             "mixed": synthetic_mixed}
+             "mixed": synthetic_mixed,
+             # the same mix with the reference's own kind of specular powers (integers: no general pow)
+             "mixed_int": lambda: synthetic_mixed(powers=(1, 4, 20))}
     key = name.lower()
     if key in table:
         return table[key]()

@@ -105,7 +105,9 @@ typedef struct rt_opts {
     int32_t first_dev;    /* first HIP device (default 0) */
     int32_t ndev;         /* devices used by rt_render in this process (default 1; -1 = all visible).
                              Test hook: the environment variable RT_DEVICE_ALIAS=N (1..4, read once
-                             per process) makes rt_render see N devices that are all first_dev */
+                             per process) makes rt_render see N devices that are all first_dev; one
+                             call then holds N of the device's 4 contexts, so the hook supports one
+                             rt_render caller at a time (concurrent callers with N >= 3 can deadlock) */
     int32_t precision;    /* RT_OUT_F64 (default) or RT_OUT_F32 */
     int32_t order;        /* RT_ORDER_EXACT (default) or RT_ORDER_FAST */
     uint32_t row_block;   /* multi-device interleave granularity in rows (default 16) */
