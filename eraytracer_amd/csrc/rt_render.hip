@@ -2329,10 +2329,13 @@ int launch_frame(rt_prepared *p, const long long (&args)[12], hipStream_t st, F 
     hipGraph_t gr = nullptr;
     const hipError_t e = hipStreamEndCapture(p->cap, &gr);
     if (rc == RT_OK && e == hipSuccess && (long long)p->gen != key[11]) {
-        // the work space or the primary masks changed while capturing: nothing was run — drop
-        // the graph and render this frame directly
+        // the work space or the primary masks changed while capturing: no device work was run —
+        // drop the graph and render this frame directly.  The host state the capture changed is
+        // reset first: primary masks computed during the capture were never written (their k_pmask
+        // launch is in the dropped graph), so the direct run must compute them again.
         (void)hipGraphDestroy(gr);
         p->last_valid = false;
+        p->pmask_valid = false;
         return enqueue(st);
     }
     if (rc != RT_OK || e != hipSuccess) {

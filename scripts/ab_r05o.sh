@@ -10,3 +10,4 @@ for rep in 1 2 3; do for v in base lid lidmix; do for sc in mixed mixed_int; do
 done; done; done
 RT_LIB_PATH=eraytracer_amd/variants/librtmi355x_lidmix.so timeout -k 10 600 python -u -m pytest tests/test_gpu_frames.py tests/test_gpu_fullsize.py tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/r05o_pytest.log 2>&1 || { tail -30 gpurun_out/r05o_pytest.log; exit 1; }; tail -2 gpurun_out/r05o_pytest.log
 REPS=3 BENCH_CFGS="c3q c5q" bash scripts/gpu_r04.sh r05p ab lidmix walkpf
+REPS=2 BENCH_CFGS="c3q c5q" bash scripts/gpu_r04.sh r05q ab walkpf l1g2560 l1g5120
