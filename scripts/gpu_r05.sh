@@ -23,9 +23,12 @@ test)
 c3)
   b c3d --steps 20 --warmup 5 --no-boundary --no-cpu-baseline || exit 1 ;;
 bench)
+  make -C oracle > /dev/null || exit 1
+  timeout -k 10 200 python scripts/cpu_config1.py > gpurun_out/${TAG}_cfg1.json && cat gpurun_out/${TAG}_cfg1.json || exit 1
   b c3d --steps 20 --warmup 5 --no-boundary --no-cpu-baseline || exit 1
   b c3 || exit 1
   b c2 $C2 --no-cpu-baseline || exit 1
+  b c4 --size 8192 --no-cpu-baseline --no-boundary || exit 1
   b c5 $C5 --steps 10 --warmup 4 --no-boundary --cpu-seconds 10 || exit 1 ;;
 prof3)
   bash scripts/profile.sh prof_${TAG}_c3 > gpurun_out/prof_${TAG}_c3.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_c3.log; exit 1; }
