@@ -4,7 +4,7 @@
 #   bash scripts/gpu_r05.sh TAG bench     bench lines: config 3 (driver-style 20/5 and default), configs 2, 5
 #   bash scripts/gpu_r05.sh TAG c3        config 3 driver-style bench line only
 #   bash scripts/gpu_r05.sh TAG prof3     rocprofv3 kernel trace + PMC passes of config 3
-#   bash scripts/gpu_r05.sh TAG prof5     the same for config 5
+#   bash scripts/gpu_r05.sh TAG prof5     the same for config 5 (prof2: config 2)
 set -o pipefail
 TAG=${1:-r05}
 PART=${2:-test}
@@ -34,6 +34,10 @@ prof3)
   bash scripts/profile.sh prof_${TAG}_c3 > gpurun_out/prof_${TAG}_c3.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_c3.log; exit 1; }
   python3 scripts/pmc_summary.py gpurun_out/prof_${TAG}_c3 gpurun_out/${TAG}_c3_pmc.json s64-4096x4096-d5-exact-f32-n1 20 20 > gpurun_out/${TAG}_c3_pmc.txt || exit 1
   grep -E "window_ns|f64_issue|wait_any_share|hbm_bytes" gpurun_out/${TAG}_c3_pmc.txt ;;
+prof2)
+  bash scripts/profile.sh prof_${TAG}_c2 $C2 > gpurun_out/prof_${TAG}_c2.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_c2.log; exit 1; }
+  python3 scripts/pmc_summary.py gpurun_out/prof_${TAG}_c2 gpurun_out/${TAG}_c2_pmc.json default-1920x1080-d5-exact-f32-n1 20 20 > gpurun_out/${TAG}_c2_pmc.txt || exit 1
+  grep -E "window_ns|f64_issue|wait_any_share|hbm_bytes" gpurun_out/${TAG}_c2_pmc.txt ;;
 prof5)
   bash scripts/profile.sh prof_${TAG}_c5 $C5 --steps 6 --warmup 3 --iso 4 > gpurun_out/prof_${TAG}_c5.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_c5.log; exit 1; }
   python3 scripts/pmc_summary.py gpurun_out/prof_${TAG}_c5 gpurun_out/${TAG}_c5_pmc.json s256-4096x4096-d8-exact-f32-n1-spp16 6 4 16 > gpurun_out/${TAG}_c5_pmc.txt || exit 1
