@@ -2117,6 +2117,15 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     // no side streams (frames in flight): each level's shading fused into the next reflection
     // pass (k_reflect_shade)
     const bool fuse = !overlap && !levels && nrefl > 0;
+    // Inline walks (k_reflect_shade's iw, levels >= 1): the chain of a shaded record without a child
+    // is walked by the kernel that shaded it, and the deepest level's hits are shaded and walked by
+    // the kernel that found them (not queued) — what k_walk did, minus its launch, the terminal
+    // records' colour entries and their re-reads.  Needs the shadow answers in the records (<= 32
+    // lights) and two reflection levels or more (level 1's kernel, the dominant one, is left as is).
+#ifndef RT_INLINE_WALK
+#define RT_INLINE_WALK 1
+#endif
+    const bool iw = RT_INLINE_WALK && fuse && p->hdr.n_light <= 32 && nrefl >= 2;
     for (int row0 = row_begin; row0 < row_end; row0 += pass_rows) {
         const int rows = std::min(pass_rows, row_end - row0);
         const int ntiles = tiles_x * ((rows + TILE - 1) / TILE);
@@ -2157,6 +2166,9 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         // level k's dense list, then its shading (k_light reads only level k: on a side stream
         // it starts as soon as the list exists and runs beside the next reflections)
         auto level_lists = [&](int k) -> int {
+            // (inline walks, depth 3: level 2 is shaded by the kernel that finds its hits, never queued;
+            // deeper frames queue their deepest level when the deep levels are sparse, decided on the device)
+            if (iw && k == nrefl && nrefl == 2) return RT_OK;
             hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k);
             HIPCHK(hipGetLastError());
             if (overlap) {
@@ -2190,11 +2202,18 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             // waves each, bound by one wave's dependent chain: they walk two candidates per step
             KtScope kt(p, k == 1 ? RT_KT_LEVEL1 : 0, st);
             if (fuse) {
-#define RT_RS(SPHV, ILPV, LDSV, BVHV)                                                                               \
-    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV>), dim3(k == 1 ? sblocks1 : sblocks), dim3(BLOCK), \
-                       LDSV, st, rhdr,                                                                              \
+#define RT_RS_(SPHV, ILPV, LDSV, BVHV, LASTV)                                                                      \
+    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV, LASTV>), dim3(k == 1 ? sblocks1 : sblocks),     \
+                       dim3(BLOCK), LDSV, st, rhdr,                                                                 \
                        p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
-                       colk(k - 1), g)
+                       colk(k - 1), g, iw && k >= 2 ? (k == nrefl ? 2 : 1) : 0)
+#define RT_RS(SPHV, ILPV, LDSV, BVHV)                                                                               \
+    do {                                                                                                           \
+        if (ILPV && iw && k == nrefl)                                                                              \
+            RT_RS_(SPHV, ILPV, LDSV, BVHV, ILPV);                                                                  \
+        else                                                                                                       \
+            RT_RS_(SPHV, ILPV, LDSV, BVHV, false);                                                                 \
+    } while (0)
                 // levels traversing the sphere BVH (unstaged scenes only): the BVH instantiations
                 const bool bvh_k = bvh_at(k);
                 if (staged && bvh_k) RT_RS(2, true, lds_r(k), true);
@@ -2207,6 +2226,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                 else if (k == 1) RT_RS(0, false, lds, false);
                 else RT_RS(0, true, lds, false);
 #undef RT_RS
+#undef RT_RS_
             } else if (lv && k == 1)
                 hipLaunchKernelGGL((k_reflect<true, false>), dim3(sblocks), dim3(BLOCK), lds, st, rhdr, p->d_tab,
                                    p->d_itab, k, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), lv, chk(k - 1), g);
@@ -2279,8 +2299,10 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[nrefl], 0));
                 HIPCHK(hipStreamWaitEvent(st, p->ev_lit[0], 0));
                 if (D > 2) walk(st, 2, D, false);
-            } else {
+            } else if (!iw) {
                 walk(st, 1, D, true); // every chain in one launch, sparse deep levels shaded there too
+            } else if (nrefl >= 3) {
+                walk(st, 2, D, true); // the sparse deep levels' chains (exits when they are dense)
             }
             HIPCHK(hipGetLastError());
         } else if (overlap && nshade > 0) {

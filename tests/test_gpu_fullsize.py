@@ -156,14 +156,21 @@ def frame(sc, w, h, d, side):
         return img.cpu().numpy()
     finally:
         L.rt_release(p)
-for name, w, h, d in [('default', 96, 72, 5), ('default_powers', 96, 72, 5), ('mixed', 128, 96, 5),
-                      ('mixed', 64, 48, 2), ('s64', 96, 96, 5), ('s256', 64, 48, 8)]:
-    sc = scenes.named(name)
+# depths 2 .. 8: the inline chain walks (k_reflect_shade's iw) start at depth 3 — there the deepest
+# level (2) is never queued, k_items and k_walk are not launched — and from depth 4 leave the sparse
+# deep levels to k_walk; 40 lights (more than a record's 32 shadow answers) keep k_walk for every chain
+cases = [(n, w, h, d) for n, w, h, d in [('default', 96, 72, 5), ('default_powers', 96, 72, 5), ('mixed', 128, 96, 5),
+                                          ('mixed', 64, 48, 2), ('mixed', 128, 96, 3), ('s64', 96, 96, 5),
+                                          ('s64', 96, 96, 3), ('s64', 96, 96, 4), ('s256', 64, 48, 8),
+                                          ('s256', 64, 48, 3)]]
+cases += [('lights40', 64, 48, 3), ('lights40', 64, 48, 4)]
+for name, w, h, d in cases:
+    sc = scenes.synthetic_scene(24, 0x5EED4040, n_lights=40) if name == 'lights40' else scenes.named(name)
     a, b = frame(sc, w, h, d, 1), frame(sc, w, h, d, 0)
     assert np.array_equal(a.view(np.int64), b.view(np.int64)), name
     ref = O.render(N.marshal(sc), w, h, d, mode=O.MEMO)
     err = np.abs(b - ref).max()
-    assert err <= 1e-5, (name, err)
+    assert err <= 1e-5, (name, d, err)
 print('fused ok')
 """
     env = dict(os.environ, RT_ENGINE="wave", PYTHONPATH=ROOT)
@@ -214,6 +221,24 @@ for name, w, h, d in [('s16', 80, 64, 5), ('s64', 96, 96, 5), ('s256', 64, 48, 8
     assert np.abs(b - ref).max() <= 1e-5, name
 print('ok')
 """, RT_ENGINE="wave", RT_BVH_MIN="2", RT_BVH_LEVEL="1")
+
+
+def test_inline_walks_dense_deep_levels():
+    """The inline chain walks with dense deep levels (more than DEEP_DENSE_RECORDS level-2 records:
+    every level shaded by its own launch, the deepest level's hits shaded where they are found, k_walk
+    left with nothing): S256 4096x2048 (about 0.7 M level-2 records) at depths 3, 4 and 6, frames in
+    flight vs the side-stream path bit for bit, and rows against the oracle."""
+    _child(r"""
+sc = scenes.s256()
+el = N.marshal(sc)
+for d in (3, 4, 6):
+    a, b = frame(sc, 4096, 2048, d, 1), frame(sc, 4096, 2048, d, 0)
+    assert np.array_equal(a.view(np.int64), b.view(np.int64)), d
+    for r in (0, 1037, 2047):
+        ref = O.render(el, 4096, 2048, d, mode=O.MEMO, row0=r, nrows=1)
+        assert np.abs(b[r:r + 1] - ref).max() <= 1e-5, (d, r)
+print('ok')
+""", RT_ENGINE="wave")
 
 
 def test_config5_rows_through_the_bvh_path(oracle):
