@@ -2052,7 +2052,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         rc = grow(reinterpret_cast<void **>(&p->d_counts), &p->counts_bytes, max_tiles * nlev * sizeof(int), &p->gen);
     const bool overlap = lit_overlap(p) && D > 1 && p->hdr.n_light > 0;
     // dense work lists: 64 per-level record counts, then per level the slots of its records in tile order
-    const size_t list0 = 64;
+    const size_t list0 = LEVEL_COUNTS;
     const size_t items_ints = list0 + slots * nlev;
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_items), &p->items_bytes, items_ints * sizeof(int), &p->gen);
@@ -2144,7 +2144,6 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         auto colk = [&](int k) { return k > 0 ? p->d_colbuf + (size_t)(k - 1) * ntiles * TILE_SLOTS * COL_W : nullptr; };
         auto chk = [&](int k) { return p->d_child + (size_t)k * ntiles * TILE_SLOTS; };
         auto litk = [&](int k) { return p->d_lit + (size_t)k * ntiles * TILE_SLOTS; };
-        HIPCHK(hipMemsetAsync(nitems, 0, list0 * sizeof(int), st));
         const dim3 iblocks((ntiles + ITEMS_BLOCK - 1) / ITEMS_BLOCK);
         const PassGeom g{W, H, rb, sh, ns, row0, spp, sample, seed, acc_p}; // level-0 records are rebuilt from it
         const dim3 grid(std::min(ntiles, PRIMARY_GRID)); // k_primary: grid-stride loop over the tiles
@@ -2153,11 +2152,11 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             if (lv0)
                 hipLaunchKernelGGL((k_primary<PREC, true>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab, W,
                                    H, D, rb, sh, ns, rows, row0, o, lv0, q, p->d_counts, ntiles, spp, sample, seed, acc_p,
-                                   pmask);
+                                   pmask, nitems);
             else
                 hipLaunchKernelGGL((k_primary<PREC, false>), grid, dim3(PRIMARY_BLOCK), 0, st, p->hdr, p->d_tab, p->d_itab,
                                    W, H, D, rb, sh, ns, rows, row0, o, lv, q, p->d_counts, ntiles, spp, sample, seed, acc_p,
-                                   pmask);
+                                   pmask, nitems);
         }
         HIPCHK(hipGetLastError());
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
