@@ -2117,11 +2117,13 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     // no side streams (frames in flight): each level's shading fused into the next reflection
     // pass (k_reflect_shade)
     const bool fuse = !overlap && !levels && nrefl > 0;
-    // Inline walks (k_reflect_shade's iw, levels >= 1): the chain of a shaded record without a child
-    // is walked by the kernel that shaded it, and the deepest level's hits are shaded and walked by
-    // the kernel that found them (not queued) — what k_walk did, minus its launch, the terminal
-    // records' colour entries and their re-reads.  Needs the shadow answers in the records (<= 32
-    // lights) and two reflection levels or more (level 1's kernel, the dominant one, is left as is).
+    // Inline walks (k_reflect_shade's iw, levels >= 1): every level is shaded by the launch that
+    // reflects it; the chain of a shaded record without a child is walked by that launch, and the
+    // deepest level's hits are shaded and walked by the launch that finds them (not queued) — what
+    // k_walk did, minus its launch, the deepest level's k_items, the terminal records' colour entries
+    // and their re-reads.  Needs the shadow answers in the records (<= 32 lights) and two reflection
+    // levels or more (level 1's kernel, the dominant one, is left as is).  For S64 the dense
+    // arrangement this implies measured the same as the sparse one (profiles/r05aa_ab_memset_dense.txt).
 #ifndef RT_INLINE_WALK
 #define RT_INLINE_WALK 1
 #endif
@@ -2165,9 +2167,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         // level k's dense list, then its shading (k_light reads only level k: on a side stream
         // it starts as soon as the list exists and runs beside the next reflections)
         auto level_lists = [&](int k) -> int {
-            // (inline walks, depth 3: level 2 is shaded by the kernel that finds its hits, never queued;
-            // deeper frames queue their deepest level when the deep levels are sparse, decided on the device)
-            if (iw && k == nrefl && nrefl == 2) return RT_OK;
+            // (inline walks: the deepest level is shaded by the launch that finds its hits, never queued)
+            if (iw && k == nrefl) return RT_OK;
             hipLaunchKernelGGL(k_items, iblocks, dim3(ITEMS_BLOCK), 0, st, ck(k), ntiles, ik(k), nitems + k);
             HIPCHK(hipGetLastError());
             if (overlap) {
@@ -2204,8 +2205,8 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
 #define RT_RS_(SPHV, ILPV, LDSV, BVHV, LASTV)                                                                      \
     hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV, LASTV>), dim3(k == 1 ? sblocks1 : sblocks),     \
                        dim3(BLOCK), LDSV, st, rhdr,                                                                 \
-                       p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k), chk(k - 1),       \
-                       colk(k - 1), g, iw && k >= 2 ? (k == nrefl ? 2 : 1) : 0)
+                       p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k),                  \
+                       iw ? nullptr : chk(k - 1), colk(k - 1), g, iw && k >= 2 ? (k == nrefl ? 2 : 1) : 0)
 #define RT_RS(SPHV, ILPV, LDSV, BVHV)                                                                               \
     do {                                                                                                           \
         if (ILPV && iw && k == nrefl)                                                                              \
@@ -2300,8 +2301,6 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                 if (D > 2) walk(st, 2, D, false);
             } else if (!iw) {
                 walk(st, 1, D, true); // every chain in one launch, sparse deep levels shaded there too
-            } else if (nrefl >= 3) {
-                walk(st, 2, D, true); // the sparse deep levels' chains (exits when they are dense)
             }
             HIPCHK(hipGetLastError());
         } else if (overlap && nshade > 0) {

@@ -19,11 +19,9 @@ USED = {
     "k_reflect_shade<1,false,2,false,false,false>": "c3 c4 (level 1)",
     "k_reflect_shade<1,false,2,true,false,false>": "c3 c4 (levels 2-3)",
     "k_reflect_shade<1,false,2,true,false,true>": "c3 c4 (level 4, LAST)",
-    "k_walk<1,false,2,true,true,true>": "c3 c4",
     "k_reflect_shade<1,false,1,false,false,false>": "c5 (level 1)",
     "k_reflect_shade<1,false,1,true,true,false>": "c5 (levels 2-6, BVH)",
     "k_reflect_shade<1,false,1,true,true,true>": "c5 (level 7, BVH, LAST)",
-    "k_walk<1,false,1,true,true,true>": "c5 (exits at once)",
 }
 
 
