@@ -28,6 +28,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -168,8 +169,13 @@ def profile_for(workload_key):
     """The committed rocprofv3 summary of the same workload (profiles/*pmc*.json, written by
     scripts/pmc_summary.py from scripts/profile.sh passes; the newest by name wins), or None.
     Supplies the measured HBM bytes per frame launch and the executed FP64 issue fraction."""
+    def tag_order(p):
+        # r05ac is newer than r05z: the round, then the tag's length, then the tag
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(p))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, os.path.basename(p))
+
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=tag_order):
         try:
             d = json.load(open(p))
         except Exception:

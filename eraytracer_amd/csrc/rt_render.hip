@@ -220,11 +220,11 @@ __device__ __forceinline__ bool sph_t(double B, double C, double A4, double &t) 
     double disc = B * B - A4 * C;
     if (!(disc >= 0.001)) return false;
     double sq = sqrt_x<FAST>(disc);
-    double t0 = (-B + sq) / 2;
-    double t1 = (-B - sq) / 2;
-    if (!((t0 >= 0) && (t1 >= 0))) return false;
-    t = (t1 < t0) ? t1 : t0; // lists:min([T0, T1])
-    return true;
+    // T0 = (-B + sq)/2, T1 = (-B - sq)/2 (:379-383) with sq > 0: T1 <= T0 after rounding too (rounding
+    // is monotonic), so lists:min([T0, T1]) is T1 (bit for bit where the two are equal) and both are
+    // >= 0 iff T1 is (NaN and infinite B or disc fail either way) — T0 is never needed
+    t = (-B - sq) / 2;
+    return t >= 0;
 }
 
 // ray_triangle_intersect/2 (:402-455), with T = O - v1 and Q = T x Edge1 given
@@ -259,10 +259,8 @@ __device__ __forceinline__ bool sph_t_wave(double B, double C, double A4, double
     t = 0.0;
     if (__ballot(ok) == 0) return false;
     const double sq = sqrt_x<FAST>(ok ? disc : 1.0);
-    const double t0 = (-B + sq) / 2;
-    const double t1 = (-B - sq) / 2;
-    t = (t1 < t0) ? t1 : t0;
-    return ok & (t0 >= 0) & (t1 >= 0);
+    t = (-B - sq) / 2; // the nearer root (sph_t)
+    return ok & (t >= 0);
 }
 
 __device__ __forceinline__ bool nearer(double t, int id, double bt, int bid) {
@@ -721,10 +719,8 @@ __device__ __forceinline__ void scan_spheres(const Scene &S, int org, const D3 &
         const bool ok0 = disc0 >= 0.001, ok1 = disc1 >= 0.001;
         if (__ballot(ok0 | ok1) == 0) continue;
         const double sq0 = sqrt_x<FAST>(ok0 ? disc0 : 1.0), sq1 = sqrt_x<FAST>(ok1 ? disc1 : 1.0);
-        const double a0 = (-B0 + sq0) / 2, b0 = (-B0 - sq0) / 2;
-        const double a1 = (-B1 + sq1) / 2, b1 = (-B1 - sq1) / 2;
-        const double t0 = (b0 < a0) ? b0 : a0, t1 = (b1 < a1) ? b1 : a1;
-        const bool h0 = ok0 & (a0 >= 0) & (b0 >= 0), h1 = two & ok1 & (a1 >= 0) & (b1 >= 0);
+        const double t0 = (-B0 - sq0) / 2, t1 = (-B1 - sq1) / 2; // the nearer roots (sph_t)
+        const bool h0 = ok0 & (t0 >= 0), h1 = two & ok1 & (t1 >= 0);
         const bool u0 = h0 & nearer(t0, id0, bt, bid);
         bt = u0 ? t0 : bt;
         bid = u0 ? id0 : bid;
@@ -1238,16 +1234,22 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
             for (;;) {
                 const bool w = !blocked && mine != 0;
                 if (__ballot(w) == 0) break;
-                const int k = chunk + (w ? __builtin_ctzll(mine) : 0);
+                // the row from the chunk's (wave-uniform) first row: one address operation per lane
+                const int lk = w ? __builtin_ctzll(mine) : 0, k = chunk + lk;
                 mine &= mine - 1;
                 RT_STAT(ST_SHADOW_ITER, 1);
-                const double2 *q = reinterpret_cast<const double2 *>(org_row<SPH>(S, org, k));
+                const double2 *q = reinterpret_cast<const double2 *>(org_row<SPH>(S, org, chunk)) + 2 * lk;
                 const double2 q01 = q[0], q23 = q[1];
-                const int id = sph_id<SPH>(S, k);
                 const double B = 2 * (sd.x * q01.x + sd.y * q01.y + sd.z * q23.x);
                 double t;
                 const bool hit = sph_t_wave<(SPH >= 1)>(B, q23.y, A4, t);
-                blocked = blocked | (w & hit & ((t < ts) | ((t == ts) & (id < c))));
+                // the candidate's list position matters only at an exact tie with the target's t*
+                // (next to never): it is read for such waves alone.  The branch is taken on the bare
+                // compare's ballot (one v_cmp, no mask materialised): a lane off the walk that equals
+                // t* by chance only takes it, and the test inside is the exact one.
+                bool blk = w & hit & (t < ts);
+                if (__ballot(t == ts) != 0) blk = blk | (w & hit & (t == ts) & (sph_id<SPH>(S, k) < c));
+                blocked = blocked | blk;
             }
             if (__all(blocked)) return false;
             continue;
