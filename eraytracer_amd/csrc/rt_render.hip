@@ -263,8 +263,18 @@ __device__ __forceinline__ bool sph_t_wave(double B, double C, double A4, double
     return ok & (t >= 0);
 }
 
+#ifndef RT_X_NEARER
+#define RT_X_NEARER 0
+#endif
+#ifndef RT_X_LEAF
+#define RT_X_LEAF 0
+#endif
 __device__ __forceinline__ bool nearer(double t, int id, double bt, int bid) {
+#if RT_X_NEARER
+    return (t < bt) | ((t == bt) & (id < bid)); // (no short circuit: no divergent branch per candidate)
+#else
     return t < bt || (t == bt && id < bid); // first in list order among equal distances (:319)
+#endif
 }
 
 struct Scene {
@@ -857,7 +867,14 @@ __device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &
         const double B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
         const double C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - c2r.y;
         double t;
+#if RT_X_LEAF
+        // one divergent block: the roots only if a lane of the leaf can hit (sph_t_wave), the update
+        // as a mask
+        const bool upd = sph_t_wave<FAST>(B, C, A4, t) & ((t < bt) | ((t == bt) & (id < bid)));
+        if (upd) {
+#else
         if (sph_t<FAST>(B, C, A4, t) && nearer(t, id, bt, bid)) {
+#endif
             bt = t;
             bid = id;
             tlim = (float)t * HI;
