@@ -263,18 +263,10 @@ __device__ __forceinline__ bool sph_t_wave(double B, double C, double A4, double
     return ok & (t >= 0);
 }
 
-#ifndef RT_X_NEARER
-#define RT_X_NEARER 0
-#endif
-#ifndef RT_X_LEAF
-#define RT_X_LEAF 0
-#endif
+// (without the short circuit — no divergent branch per candidate — measured config 3 +0.9 %, config 5
+// -0.7 %: profiles/r05af_ab_nearer_no_short_circuit.txt)
 __device__ __forceinline__ bool nearer(double t, int id, double bt, int bid) {
-#if RT_X_NEARER
-    return (t < bt) | ((t == bt) & (id < bid)); // (no short circuit: no divergent branch per candidate)
-#else
     return t < bt || (t == bt && id < bid); // first in list order among equal distances (:319)
-#endif
 }
 
 struct Scene {
@@ -867,14 +859,9 @@ __device__ __forceinline__ void scan_bvh(const Scene &S, const D3 &o, const D3 &
         const double B = 2 * (d.x * oc.x + d.y * oc.y + d.z * oc.z);
         const double C = oc.x * oc.x + oc.y * oc.y + oc.z * oc.z - c2r.y;
         double t;
-#if RT_X_LEAF
-        // one divergent block: the roots only if a lane of the leaf can hit (sph_t_wave), the update
-        // as a mask
-        const bool upd = sph_t_wave<FAST>(B, C, A4, t) & ((t < bt) | ((t == bt) & (id < bid)));
-        if (upd) {
-#else
+        // (as one divergent block — sph_t_wave and the nearer test as a mask — measured neutral:
+        // profiles/r05ag_ab_bvh_leaf_block.txt)
         if (sph_t<FAST>(B, C, A4, t) && nearer(t, id, bt, bid)) {
-#endif
             bt = t;
             bid = id;
             tlim = (float)t * HI;
