@@ -1235,6 +1235,8 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
 #ifdef RT_ABL_NO_OCC // timing ablation builds only (results wrong): no occluder tests
             mine = 0;
 #endif
+            // (software-pipelined — the next candidate's row loaded while the current one is tested —
+            // measured config 5 +4 %, config 3 +1.3 %: profiles/r05ai_ab_occluder_prefetch.txt)
             for (;;) {
                 const bool w = !blocked && mine != 0;
                 if (__ballot(w) == 0) break;
