@@ -418,6 +418,11 @@ __device__ __forceinline__ double wave_max(double v) {
     return wave_reduce(v, [](double a, double b) { return fmax(a, b); });
 }
 // every lane holds the same v: keep it in SGPRs
+__device__ __forceinline__ unsigned long long uniform_u64(unsigned long long b) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
 __device__ __forceinline__ double uniform(double v) {
     unsigned long long b = (unsigned long long)__double_as_longlong(v);
     unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
@@ -1044,7 +1049,10 @@ __device__ __forceinline__ void nearest_pair(const Scene &S, int org, const D3 &
     if (!pm) b = make_beam_pair32(h, a0, d0, a1, d1);
     RT_STAT(ST_NEAR_PRE, 1);
     for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
-        unsigned long long m = pm ? pm[chunk >> 6] : b.on ? cull_chunk32_org(S, b, chunk, org) : chunk_all(h.n_sph, chunk);
+        // (the table's entry is the wave's: read as a uniform value, so the candidate walk below is a
+        // wave-uniform loop over scalar-loaded rows — read per lane, the compiler made it a per-lane walk
+        // over gathered rows: k_primary's frames 1.4-1.7 % slower, profiles/r05al_ab_uniform_primary_masks.txt)
+        unsigned long long m = pm ? uniform_u64(pm[chunk >> 6]) : b.on ? cull_chunk32_org(S, b, chunk, org) : chunk_all(h.n_sph, chunk);
         RT_STAT(ST_NEAR_PRE_CAND, __popcll(m));
         while (m) {
             const int k = chunk + __builtin_ctzll(m);
