@@ -2183,6 +2183,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         const int sblocks = std::min<int>(STRIDE_BLOCKS, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
         const int sblocks1 = std::min<int>(STRIDE_BLOCKS_L1, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
         const int sblocksw = std::min<int>(STRIDE_BLOCKS_WALK, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
+        const int sblocksb = std::min<int>(STRIDE_BLOCKS_BVH, (ntiles * (TILE_SLOTS / 64) + BLOCK / 64 - 1) / (BLOCK / 64));
         // level k's dense list, then its shading (k_light reads only level k: on a side stream
         // it starts as soon as the list exists and runs beside the next reflections)
         auto level_lists = [&](int k) -> int {
@@ -2222,7 +2223,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
             KtScope kt(p, k == 1 ? RT_KT_LEVEL1 : 0, st);
             if (fuse) {
 #define RT_RS_(SPHV, ILPV, LDSV, BVHV, LASTV)                                                                      \
-    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV, LASTV>), dim3(k == 1 ? sblocks1 : sblocks),     \
+    hipLaunchKernelGGL((k_reflect_shade<PREC, GENPOW, SPHV, ILPV, BVHV, LASTV>), dim3(k == 1 ? sblocks1 : BVHV ? sblocksb : sblocks), \
                        dim3(BLOCK), LDSV, st, rhdr,                                                                 \
                        p->d_tab, p->d_itab, k, o, qk(k - 1), ik(k - 1), nitems + (k - 1), qk(k), ck(k),                  \
                        iw ? nullptr : chk(k - 1), colk(k - 1), g, iw && k >= 2 ? (k == nrefl ? 2 : 1) : 0)
