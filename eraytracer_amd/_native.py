@@ -24,7 +24,6 @@ RT_ERANGE = -6
 RT_CAMERA, RT_POINT_LIGHT, RT_SPHERE, RT_TRIANGLE, RT_PLANE, RT_OTHER = range(6)
 RT_OUT_F64, RT_OUT_F32 = 0, 1
 RT_ORDER_EXACT, RT_ORDER_FAST = 0, 1
-RT_MAX_DEPTH = 16
 RT_MAX_SHARDS = 64
 RT_CFG_SIDE_STREAMS = 1
 RT_CFG_KERNEL_TIMING = 2

@@ -482,7 +482,6 @@ int rt_render(const rt_elem *scene, uint32_t n, uint32_t width, uint32_t height,
     if (width == 0 && height == 0) return RT_DONE;
     if (width == 0 || height == 0) return RT_EBADARG;
     if (!out_rgb) return RT_EBADARG;
-    if (depth > RT_MAX_DEPTH) return RT_ETOOBIG;
     rt_opts o;
     std::memset(&o, 0, sizeof(o));
     o.ndev = 1;

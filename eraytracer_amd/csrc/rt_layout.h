@@ -54,6 +54,11 @@ constexpr int OBJ_META_W = 4; // kind, local index within its type, canon compac
 constexpr int OCC_CELLS = RT_OCC_CELLS;
 constexpr float OCC_CELL_EPS = 1.0e-4f; // cells overlap by this much (unit-vector components)
 constexpr int OCC_CELLS_MIN_SPHERES = 128; // smaller scenes keep one cell
+// Occluder masks cost the host one test per (light, target, sphere) triple: above this many the
+// scene has none (SceneHdr::occ_ok = 0; shadow cones instead).  Above OCC_MAX_BYTES of masks,
+// one cell.
+constexpr double OCC_MAX_TESTS = 16777216.0; // 2^24: S2048 with 4 lights (~1.3 s of host time)
+constexpr double OCC_MAX_BYTES = 64.0 * 1024 * 1024;
 
 constexpr int LDS_STAGE_MAX = 32 * 1024; // 5 workgroups per CU keep their 32 KiB each
 
@@ -64,10 +69,11 @@ constexpr int LDS_STAGE_MAX = 32 * 1024; // 5 workgroups per CU keep their 32 Ki
 // for a sphere child, the sphere's compact object id.
 constexpr int BVH_NODE_DOUBLES = 8;  // 64 bytes
 constexpr int BVH_LDS_MAX = 40 * 1024; // nodes + sphere rows staged in LDS up to this size
-constexpr int BVH_STACK = 12;        // per-lane traversal stack entries (tree depth <= BVH_STACK: 4096 spheres)
+constexpr int BVH_STACK = 18;        // per-lane traversal stack entries (tree depth <= BVH_STACK)
+constexpr int BVH_MAX_SPHERES = 1 << 16; // the stack words hold 16-bit node links: more spheres, no BVH
 constexpr int BVH_MIN_SPHERES = 128; // below this the wave beams are cheaper (default; RT_BVH_MIN)
 constexpr int BVH_LEVEL = 2;         // first reflection level traversing the BVH (default; RT_BVH_LEVEL)
-constexpr int BVH_SAH_SLACK = 2;     // SAH trees may be this much deeper than ceil(log2 n_sph) (RT_BVH_SAH_SLACK)
+constexpr int BVH_SAH_SLACK = 2;     // SAH trees may be this much deeper than ceil(log2 n_sph) (compile-time)
 constexpr double BVH_BOX_REL = 1.0e-5; // box inflation, relative to the scene extent (+1)
 
 enum ObjKind : int { K_SPHERE = 0, K_TRIANGLE = 1, K_PLANE = 2 };
@@ -92,6 +98,7 @@ struct SceneHdr {
     // itab[i_occ + 2*(((i*n_sph + t)*occ_cells + e)*n_chunk + k)] has bit j set iff sphere 64k+j
     // can block a shadow ray from light i into cell e of the cone towards sphere t (rt_scene.cpp).
     int i_occ, n_chunk, occ_cells;
+    int occ_ok; // the occluder masks exist (cull_ok, spheres, and within OCC_MAX_TESTS)
     // LDS staging (spheres-only scenes with culling whose per-lane-gathered tables fit
     // LDS_STAGE_MAX bytes; l_bytes = 0 otherwise): byte offsets in the workgroup's dynamic LDS of
     // the object rows (o_obj), object meta rows (i_obj_meta), the lights' per-origin sphere rows

@@ -1227,7 +1227,7 @@ __device__ __forceinline__ bool lit_by(const Scene &S, int light, const Target &
     // Candidate occluders.  Sphere targets: the union of the host-precomputed occluder masks of
     // the wave's distinct targets (no reductions).  Otherwise the cone from the light to the
     // hit ball of the wave, culled lane-parallel.
-    const bool sph_targets = SPH || (h.cull_ok && __ballot(!blocked && kind != K_SPHERE) == 0);
+    const bool sph_targets = SPH || (h.occ_ok && __ballot(!blocked && kind != K_SPHERE) == 0);
     double tmax = __builtin_inf();
     Beam b;
     b.on = false;
@@ -1335,7 +1335,8 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
     HitBall hb;
     hb.on = false;
     hb.cx = hb.cy = hb.cz = hb.r = 0.0;
-    if (!SPH && !NB && __ballot(active && T.kind != K_SPHERE) != 0) hb = make_hitball(h, active, hit);
+    // (and for every target when the scene has no occluder masks: occ_ok = 0)
+    if (!SPH && !NB && (!h.occ_ok || __ballot(active && T.kind != K_SPHERE) != 0)) hb = make_hitball(h, active, hit);
     RT_STAT(ST_SHADE, 1);
     D3 F = {0.0, 0.0, 0.0};
     for (int i = 0; i < h.n_light; ++i) {
@@ -1518,7 +1519,7 @@ __global__ __launch_bounds__(256, NB ? RT_FUSED_NB_WAVES : RT_WAVES_PER_SIMD) vo
         float *o = reinterpret_cast<float *>(out) + pix * 3;
         o[0] = (float)col.x; o[1] = (float)col.y; o[2] = (float)col.z;
     }
-    if (LEVELS) levels[pix] = (uint8_t)(levels_hit ? (nlev > 0) : nlev);
+    if (LEVELS) levels[pix] = (uint8_t)(levels_hit ? (nlev > 0) : min(nlev, 255)); // (counts saturate at 255)
 }
 
 #include "rt_wave.inc" // the wavefront engine (default)
@@ -1607,8 +1608,8 @@ struct rt_prepared {
     // 11 Gpx/s; 3 side streams were no faster than 2 — the chip is saturated in the overlap)
     hipStream_t side[2] = {};
     int side_mode = -1; // rt_configure(RT_CFG_SIDE_STREAMS): -1 = environment (RT_LIT_STREAM), 0 off, 1 on
-    hipEvent_t ev_level[RT_MAX_DEPTH + 1] = {}; // level k's list is ready
-    hipEvent_t ev_lit[RT_MAX_DEPTH + 1] = {};   // level k is shaded
+    std::vector<hipEvent_t> ev_level; // level k's list is ready (depth + 1 of them, grown with the depth)
+    std::vector<hipEvent_t> ev_lit;   // level k is shaded
     // Frames repeat with identical arguments (bench, multi-GPU renderer): the second identical
     // rt_launch captures the frame's launch sequence into a graph, later ones replay it.
     // gen counts changes that invalidate a captured frame: work-space reallocations (captured
@@ -1662,6 +1663,7 @@ void apply_cull(rt_prepared *p) {
     p->hdr = p->hdr_full;
     if (!p->cull) {
         p->hdr.cull_ok = 0;
+        p->hdr.occ_ok = 0;
         p->hdr.beam_ok = 0;
         p->hdr.bvh_ok = 0;
         p->hdr.l_bytes = 0;
@@ -1994,13 +1996,23 @@ bool lit_overlap(const rt_prepared *p) {
     return p->side_mode < 0 ? env_on : p->side_mode != 0;
 }
 
-int side_stream(rt_prepared *p) {
-    if (p->side[0]) return RT_OK;
-    int least = 0, greatest = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    for (hipStream_t &x : p->side) HIPCHK(hipStreamCreateWithPriority(&x, hipStreamNonBlocking, least));
-    for (hipEvent_t &e : p->ev_level) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (hipEvent_t &e : p->ev_lit) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+// The side streams and one pair of level events per level 0 .. depth (created once, grown with the depth).
+int side_stream(rt_prepared *p, int depth) {
+    if (!p->side[0]) {
+        int least = 0, greatest = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        for (hipStream_t &x : p->side) HIPCHK(hipStreamCreateWithPriority(&x, hipStreamNonBlocking, least));
+    }
+    while (p->ev_level.size() < (size_t)depth + 1) {
+        hipEvent_t a = nullptr, b = nullptr;
+        HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+        if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+            (void)hipEventDestroy(a);
+            return RT_EHIP;
+        }
+        p->ev_level.push_back(a);
+        p->ev_lit.push_back(b);
+    }
     return RT_OK;
 }
 
@@ -2071,11 +2083,11 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
         rc = grow(reinterpret_cast<void **>(&p->d_counts), &p->counts_bytes, max_tiles * nlev * sizeof(int), &p->gen);
     const bool overlap = lit_overlap(p) && D > 1 && p->hdr.n_light > 0;
     // dense work lists: 64 per-level record counts, then per level the slots of its records in tile order
-    const size_t list0 = LEVEL_COUNTS;
+    const size_t list0 = level_counts(nlev);
     const size_t items_ints = list0 + slots * nlev;
     if (rc == RT_OK)
         rc = grow(reinterpret_cast<void **>(&p->d_items), &p->items_bytes, items_ints * sizeof(int), &p->gen);
-    if (rc == RT_OK && overlap) rc = side_stream(p);
+    if (rc == RT_OK && overlap) rc = side_stream(p, D);
     if (rc != RT_OK) return rc;
     // the primary rays' candidate masks of the whole slab (k_pmask), recomputed only when the
     // frame geometry or the scene changed (or after rt_trim)
@@ -2113,7 +2125,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     const int nshade = D > 0 ? 1 + nrefl : 0;
     // spheres only, culling on: every shadow target has occluder masks (lit_by<1>); their
     // per-lane-gathered tables staged in each workgroup's LDS when they fit (SPH = 2)
-    const bool sph_only = p->hdr.n_tri == 0 && p->hdr.n_pl == 0 && p->hdr.cull_ok;
+    const bool sph_only = p->hdr.n_tri == 0 && p->hdr.n_pl == 0 && p->hdr.cull_ok && p->hdr.occ_ok;
     const bool staged = sph_only && p->hdr.l_bytes > 0;
     const size_t lds = staged ? (size_t)p->hdr.l_bytes : 0;
     // Reflection kernels of levels that traverse the sphere BVH: after the staged tables in LDS,
@@ -2403,7 +2415,12 @@ int launch_frame(rt_prepared *p, const long long (&args)[12], hipStream_t st, F 
 // objects), and spheres-only scenes with LDS-staged tables at any size (below).
 // RT_ENGINE=fused | wave forces one.
 constexpr int FUSED_MAX_OBJECTS = 40;
-bool use_mega_engine(const rt_prepared *p) {
+// The fused kernel's reference-order chain keeps each level's (t, object) per pixel in LDS (12 bytes
+// per level and pixel): deeper frames in reference order take the wavefront engine, whose per-level
+// queues are sized at run time (rt_render.hip launch_wavefront).
+constexpr int FUSED_MAX_DEPTH = 16;
+bool use_mega_engine(const rt_prepared *p, int depth = 0, int order = RT_ORDER_EXACT) {
+    if (order == RT_ORDER_EXACT && depth > FUSED_MAX_DEPTH) return false;
     static const int mode = [] { // 0 auto, 1 fused, 2 wave
         const char *s = std::getenv("RT_ENGINE");
         if (s && (std::strcmp(s, "fused") == 0 || std::strcmp(s, "mega") == 0)) return 1;
@@ -2453,7 +2470,6 @@ int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dep
     if (!p || !d_out) return RT_EBADARG;
     if (width == 0 && height == 0) return RT_DONE;
     if (width == 0 || height == 0) return RT_EBADARG;
-    if (depth > RT_MAX_DEPTH) return RT_ETOOBIG;
     if (row_block == 0 || nshards == 0 || shard >= nshards) return RT_EBADARG;
     if (precision != RT_OUT_F64 && precision != RT_OUT_F32) return RT_EBADARG;
     if (order != RT_ORDER_EXACT && order != RT_ORDER_FAST) return RT_EBADARG;
@@ -2508,7 +2524,7 @@ int rt_launch_rows(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dep
         }
         return RT_OK;
     }
-    if (!use_mega_engine(p)) { // the wavefront engine always evaluates the reference's exact order
+    if (!use_mega_engine(p, D, order)) { // the wavefront engine always evaluates the reference's exact order
         const long long key[12] = {W, H, D, rb, sh, ns, precision, ((long long)r0 << 32) | r1,
                                    (long long)(intptr_t)d_out, (long long)(intptr_t)d_levels, levels_hit, 0};
         return launch_frame(p, key, st, [&](hipStream_t s) {

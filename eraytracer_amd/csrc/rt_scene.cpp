@@ -55,35 +55,59 @@ static size_t payload_bytes(int kind) {
     }
 }
 
+// No count limits: the reference's scans take any list (nearest_object_intersecting_ray/6,
+// raytracer.erl:300-346; lighting_function/6 folds over every light, :209-252).  What does not
+// fit the device (or the 32-bit table offsets) fails with RT_ENOMEM in compile_scene.
 int check_scene(const rt_elem *e, uint32_t n) {
     if (!e || n < 1) return RT_EBADARG;         // [Camera|Rest] must match (raytracer.erl:180)
     if (e[0].kind != RT_CAMERA) return RT_EBADARG; // Camera#camera.location would crash (:488)
-    uint32_t nobj = 0, nl = 0;
+    if (n > (uint32_t)INT32_MAX / 2) return RT_ENOMEM; // object ids are 32-bit ints in the kernels
     for (uint32_t i = 0; i < n; i++) {
         if (!elem_ok(e[i])) return RT_EBADARG;
         if (e[i].canon < -1 || e[i].canon > (int32_t)i) return RT_EBADARG;
         if (e[i].canon >= 0 && e[e[i].canon].kind != e[i].kind) return RT_EBADARG;
-        if (i == 0) continue;
-        if (e[i].kind == RT_SPHERE || e[i].kind == RT_TRIANGLE || e[i].kind == RT_PLANE) nobj++;
-        if (e[i].kind == RT_POINT_LIGHT) nl++;
     }
-    if (nobj > RT_MAX_OBJECTS || nl > RT_MAX_LIGHTS) return RT_ETOOBIG;
     return RT_OK;
 }
 
+// canon[i] = the first j <= i of the same kind that is its own canonical element and has the same
+// payload bytes.  One hash lookup per element (the elements so far that are their own canonical
+// element, keyed by kind and payload; the first one of each key kept), not a scan of the prefix.
 int fill_canon(rt_elem *e, uint32_t n) {
     if (!e) return RT_EBADARG;
-    for (uint32_t i = 0; i < n; i++) {
-        if (e[i].canon >= 0) continue;
-        e[i].canon = (int32_t)i;
-        size_t nb = payload_bytes(e[i].kind);
-        for (uint32_t j = 0; j < i; j++) {
-            if (e[j].kind == e[i].kind && (int32_t)j == e[j].canon && nb &&
-                std::memcmp(&e[j].u, &e[i].u, nb) == 0) {
-                e[i].canon = (int32_t)j;
-                break;
+    struct Key {
+        const rt_elem *p;
+        size_t nb;
+    };
+    auto hash = [](const rt_elem *p, size_t nb) {
+        uint64_t h = 1469598103934665603ull ^ (uint64_t)(uint32_t)p->kind;
+        const unsigned char *b = reinterpret_cast<const unsigned char *>(&p->u);
+        for (size_t k = 0; k < nb; ++k) h = (h ^ b[k]) * 1099511628211ull;
+        return h;
+    };
+    // open addressing over indices (-1 = empty); 2x the element count, a power of two
+    size_t cap = 16;
+    while (cap < 2 * (size_t)n) cap <<= 1;
+    std::vector<int32_t> slot(cap, -1);
+    auto find_or_add = [&](uint32_t i, bool add) -> int32_t {
+        const size_t nb = payload_bytes(e[i].kind);
+        size_t s = hash(&e[i], nb) & (cap - 1);
+        for (;; s = (s + 1) & (cap - 1)) {
+            const int32_t j = slot[s];
+            if (j < 0) {
+                if (add) slot[s] = (int32_t)i;
+                return -1;
             }
+            if (e[j].kind == e[i].kind && std::memcmp(&e[j].u, &e[i].u, nb) == 0) return j;
         }
+    };
+    for (uint32_t i = 0; i < n; i++) {
+        const bool has = payload_bytes(e[i].kind) != 0; // RT_OTHER terms are never matched
+        if (e[i].canon < 0) {
+            const int32_t j = has ? find_or_add(i, false) : -1;
+            e[i].canon = j >= 0 ? j : (int32_t)i;
+        }
+        if (has && e[i].canon == (int32_t)i) (void)find_or_add(i, true); // keeps the first of its key
     }
     return RT_OK;
 }
@@ -142,7 +166,7 @@ static void build_bvh(const std::vector<rt_elem> &e, const std::vector<int> &sph
         return s ? std::atoi(s) : BVH_LEVEL; // level 1 (coherent: from the primary hits) keeps the beams
     }();
     const int n = (int)sph.size();
-    if (!h.cull_ok || n < 2 || n < bvh_min) return;
+    if (!h.cull_ok || n < 2 || n < bvh_min || n > BVH_MAX_SPHERES) return;
     int depth = 0;
     while ((1 << depth) < n) ++depth;
     if (depth > BVH_STACK) return; // a node at depth i holds at most i stack entries, pushes one more
@@ -318,6 +342,13 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
         } else if (k == RT_POINT_LIGHT) {
             lights.push_back((int)i);
         }
+    }
+    // The per-origin tables (camera and every light) hold ~16 doubles per (origin, sphere) pair: a
+    // scene whose tables would not fit 32-bit offsets is refused before they are built.
+    {
+        const double per_origin = 16.0 * (double)objs.size();
+        if ((double)(1 + lights.size()) * per_origin + 32.0 * (double)objs.size() >= (double)INT32_MAX / 2)
+            return RT_ENOMEM;
     }
     std::vector<int> sph, tri, pl;
     for (int i : objs) {
@@ -549,18 +580,18 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
     for (int i : pl) it.push_back(compact[i]);
     while (it.size() % 4) it.push_back(0); // 16-byte rows
     h.i_obj_meta = (int)it.size();
-    for (int i : objs) {
-        int kind = e[i].kind == RT_SPHERE ? K_SPHERE : (e[i].kind == RT_TRIANGLE ? K_TRIANGLE : K_PLANE);
-        const std::vector<int> &grp = kind == K_SPHERE ? sph : (kind == K_TRIANGLE ? tri : pl);
-        // the canonical (first exactly equal) element is a record of the same type: its index
-        // within the type is stored here too, so a shadow target resolves in one load
-        const int r = root(e, i);
-        int local = 0, rlocal = 0;
-        for (size_t q = 0; q < grp.size(); q++) {
-            if (grp[q] == i) local = (int)q;
-            if (grp[q] == r) rlocal = (int)q;
+    {
+        // each element's index within its type's table
+        std::vector<int> local_of(n, 0);
+        for (const std::vector<int> *grp : {&sph, &tri, &pl})
+            for (size_t q = 0; q < grp->size(); q++) local_of[(*grp)[q]] = (int)q;
+        for (int i : objs) {
+            int kind = e[i].kind == RT_SPHERE ? K_SPHERE : (e[i].kind == RT_TRIANGLE ? K_TRIANGLE : K_PLANE);
+            // the canonical (first exactly equal) element is a record of the same type: its index
+            // within the type is stored here too, so a shadow target resolves in one load
+            const int r = root(e, i);
+            it.insert(it.end(), {kind, local_of[i], compact[r], local_of[r]});
         }
-        it.insert(it.end(), {kind, local, compact[r], rlocal});
     }
     // Occluder masks, per (light, target sphere, direction cell).  Shadow rays to a target
     // sphere t start at the light L and point into the cone from L around ball(c_t, r_t); the
@@ -580,10 +611,17 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
     // than they save (measured: config 3 -5 %); large scenes get OCC_CELLS (config 5: +4 %).
     const bool stage_kind = h.cull_ok && h.n_tri == 0 && h.n_pl == 0 && h.n_sph > 0 && h.n_light > 0;
     h.occ_cells = (h.n_sph < OCC_CELLS_MIN_SPHERES || (stage_kind && stage_bytes(h, 1) <= LDS_STAGE_MAX)) ? 1 : OCC_CELLS;
+    // The masks cost the host one (light, target, sphere) test per triple and the device
+    // n_light * n_sph^2 * cells bits: beyond OCC_MAX_TESTS tests there are none (occ_ok = 0) and
+    // the shadow rays take the shadow cones over the sphere chunks instead (lit_by); beyond
+    // OCC_MAX_BYTES the masks keep one cell.
+    const double occ_tests = (double)h.n_light * h.n_sph * h.n_sph;
+    h.occ_ok = h.cull_ok && h.n_sph > 0 && occ_tests <= OCC_MAX_TESTS ? 1 : 0;
+    if (h.occ_ok && (double)h.n_light * h.n_sph * h.occ_cells * h.n_chunk * 8 > OCC_MAX_BYTES) h.occ_cells = 1;
     const int ncell = h.occ_cells;
     while (it.size() % 2) it.push_back(0);
     h.i_occ = (int)it.size();
-    if (h.cull_ok && h.n_sph > 0) {
+    if (h.occ_ok) {
         for (int li : lights) {
             const rt_vec3 &L = e[li].u.point_light.location;
             for (int ti : sph) {
@@ -677,6 +715,8 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
         }
     }
     if (it.empty()) it.push_back(0);
+    // the kernels index both tables with 32-bit ints
+    if (t.size() >= (size_t)INT32_MAX / 2 || it.size() >= (size_t)INT32_MAX / 2) return RT_ENOMEM;
 
     // camera: point_on_screen/3 (:486-503) with focal_length/2 (:483-484).
     // Sum = foldl(fun(V, S) -> vector_add(V, S) end, Location, [ {0*F,0*F,1*F}, {(X-0.5)*SW,0,0},
@@ -705,7 +745,7 @@ int compile_scene(const rt_elem *in, uint32_t n, Compiled &out) {
     // LDS staging layout (16-byte aligned sections)
     h.l_obj = h.l_meta = h.l_org = h.l_occ = h.l_id = h.l_sphb = -1;
     h.l_bytes = 0;
-    if (stage_kind && h.occ_cells == 1) {
+    if (stage_kind && h.occ_ok && h.occ_cells == 1) {
         auto up16 = [](long v) { return (v + 15) / 16 * 16; };
         long off = 0;
         const long l_obj = off; off = up16(off + (long)h.n_obj * OBJ_W * 8);

@@ -48,8 +48,8 @@ def _sizes_ok(width, height):
 def _depth_ok(depth):
     if isinstance(depth, bool) or not isinstance(depth, int) or depth < 0:
         raise ValueError(f"badarg: Recursion_depth must be a non-negative integer, got {depth!r}")
-    if depth > N.RT_MAX_DEPTH:
-        raise ValueError(f"badarg: Recursion_depth {depth} exceeds the library limit {N.RT_MAX_DEPTH}")
+    if depth >= 1 << 32:  # the C ABI's uint32_t (no other depth limit: RT_ENOMEM when it does not fit)
+        raise ValueError(f"badarg: Recursion_depth {depth} does not fit the library's 32-bit depth")
 
 
 def render(width: int, height: int, scene=None, depth: int = 5, *, precision: str = "f64",

@@ -141,7 +141,12 @@ def named(name: str):
     key = name.lower()
     if key in table:
         return table[key]()
-    if key.startswith("s") and key[1:].isdigit() and 1 <= int(key[1:]) <= 4000:
-        n = int(key[1:])  # sN: N spheres, seed 0x5EED<N as four decimal digits> like S64 / S256
+    if key.startswith("s") and key[1:].isdigit() and 1 <= int(key[1:]) <= 1 << 20:
+        n = int(key[1:])  # sN: N spheres, seed 0x5EED<N as (at least) four decimal digits> like S64 / S256
         return synthetic_scene(n, int(f"5EED{n:04d}", 16))
+    if key.startswith("s") and "l" in key[1:]:
+        a, b = key[1:].split("l", 1)  # sNlM: sN with M lights (seed as sN's)
+        if a.isdigit() and b.isdigit() and 1 <= int(a) <= 1 << 20 and 0 <= int(b) <= 1 << 16:
+            n = int(a)
+            return synthetic_scene(n, int(f"5EED{n:04d}", 16), n_lights=int(b))
     raise ValueError(f"unknown scene {name!r}; expected one of {sorted(table)} or sN")

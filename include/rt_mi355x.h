@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* ---- return codes ------------------------------------------------------- */
 #define RT_OK 0
@@ -46,12 +46,16 @@ extern "C" {
 #define RT_ENODEV (-2)     /* no HIP device, or device index out of range */
 #define RT_EHIP (-3)       /* a HIP runtime call failed */
 #define RT_ENOMEM (-4)     /* host or device allocation failed */
-#define RT_ETOOBIG (-5)    /* size exceeds a documented limit (see RT_MAX_*) */
+#define RT_ETOOBIG (-5)    /* a frame size, spp or shard count above its documented limit (RT_MAX_*) */
 #define RT_ERANGE (-6)     /* rt_ppm_format: a channel below -2^31 after scaling (see there) */
 
-#define RT_MAX_DEPTH 16    /* recursion depths above this are rejected */
-#define RT_MAX_OBJECTS 4096
-#define RT_MAX_LIGHTS 64
+/* No limit on the recursion depth or on the number of objects or lights: the reference recurses
+ * to any depth (pixel_colour_from_ray/3, raytracer.erl:186-203), folds over every light
+ * (lighting_function/6, :209-252) and scans any list (nearest_object_intersecting_ray/6,
+ * :300-346).  Frames whose work space (per-level hit queues, ~100 bytes per pixel and level, in
+ * row passes of at least 16 rows) or scene tables (32-bit offsets: about 16 doubles per
+ * (origin, object) pair, the origins being the camera and every light) do not fit fail with
+ * RT_ENOMEM.  out_levels saturates at 255. */
 
 /* ---- scene records, mirroring the reference's records (raytracer.erl:72-81) -- */
 enum rt_kind {

@@ -410,7 +410,7 @@ static void *worker(void *arg) {
             }
             size_t o = ((size_t)r * j->W + x);
             j->out[o * 3 + 0] = c.x; j->out[o * 3 + 1] = c.y; j->out[o * 3 + 2] = c.z;
-            if (j->levels) j->levels[o] = (uint8_t)lv;
+            if (j->levels) j->levels[o] = (uint8_t)(lv > 255 ? 255 : lv); /* saturating, as rt_opts.out_levels */
         }
     }
     return NULL;

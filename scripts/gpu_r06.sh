@@ -1,0 +1,50 @@
+#!/bin/bash
+# Round-6 GPU steps (each under its own time limit; the first failure ends the call).
+#   bash scripts/gpu_r06.sh TAG lim       the input-size tests (depth, lights, objects) alone
+#   bash scripts/gpu_r06.sh TAG test      GPU parity suite, then the RT_DEBUG_LISTS build's wavefront tests
+#   bash scripts/gpu_r06.sh TAG bench     bench lines: config 3 (driver-style 20/5 and default), configs 2, 5
+#   bash scripts/gpu_r06.sh TAG c3        config 3 driver-style bench line only
+#   bash scripts/gpu_r06.sh TAG prof3     rocprofv3 kernel trace + PMC passes of config 3
+#   bash scripts/gpu_r06.sh TAG prof5     the same for config 5 (prof2: config 2)
+set -o pipefail
+TAG=${1:-r06}
+PART=${2:-test}
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+C2="--scene default --width 1920 --height 1080 --depth 5"
+C5="--scene s256 --depth 8 --spp 16"
+b() { name=$1; shift; timeout -k 10 300 python bench.py "$@" > gpurun_out/${TAG}_bench_$name.json 2> gpurun_out/${TAG}_bench_$name.err || { tail -5 gpurun_out/${TAG}_bench_$name.err; exit 1; }; python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], d['value'], 'Mpx/s', d['ms_per_step'], 'ms/frame', 'dom', r.get('launch_ms_live'), 'frac', r.get('frac'), 'cpu', d.get('cpu_baseline', {}).get('value'), d.get('cpu_baseline', {}).get('cores'))" gpurun_out/${TAG}_bench_$name.json $name; }
+case $PART in
+lim)
+  make -C oracle > /dev/null || exit 1
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_limits.py -x -v -m gpu --timeout 400 --timeout-method thread > gpurun_out/pytest_lim_$TAG.log 2>&1 || { tail -40 gpurun_out/pytest_lim_$TAG.log; exit 1; }
+  grep -E "PASS|FAIL|depth|passed|failed" gpurun_out/pytest_lim_$TAG.log | tail -20 ;;
+test)
+  make -C oracle > /dev/null || exit 1
+  timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_$TAG.log; exit 1; }
+  tail -1 gpurun_out/pytest_$TAG.log
+  bash scripts/debug_lists.sh run > gpurun_out/debug_lists_$TAG.log 2>&1 || { tail -30 gpurun_out/debug_lists_$TAG.log; exit 1; }
+  tail -1 gpurun_out/debug_lists_$TAG.log ;;
+c3)
+  b c3d --steps 20 --warmup 5 --no-boundary --no-cpu-baseline || exit 1 ;;
+bench)
+  make -C oracle > /dev/null || exit 1
+  timeout -k 10 200 python scripts/cpu_config1.py > gpurun_out/${TAG}_cfg1.json && cat gpurun_out/${TAG}_cfg1.json || exit 1
+  b c3d --steps 20 --warmup 5 --no-boundary --no-cpu-baseline || exit 1
+  b c3 || exit 1
+  b c2 $C2 --no-cpu-baseline || exit 1
+  b c4 --size 8192 --no-cpu-baseline --no-boundary || exit 1
+  b c5 $C5 --steps 10 --warmup 4 --no-boundary --cpu-seconds 10 || exit 1 ;;
+prof3)
+  bash scripts/profile.sh prof_${TAG}_c3 > gpurun_out/prof_${TAG}_c3.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_c3.log; exit 1; }
+  python3 scripts/pmc_summary.py gpurun_out/prof_${TAG}_c3 gpurun_out/${TAG}_c3_pmc.json s64-4096x4096-d5-exact-f32-n1 20 20 > gpurun_out/${TAG}_c3_pmc.txt || exit 1
+  grep -E "window_ns|f64_issue|wait_any_share|hbm_bytes" gpurun_out/${TAG}_c3_pmc.txt ;;
+prof2)
+  bash scripts/profile.sh prof_${TAG}_c2 $C2 > gpurun_out/prof_${TAG}_c2.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_c2.log; exit 1; }
+  python3 scripts/pmc_summary.py gpurun_out/prof_${TAG}_c2 gpurun_out/${TAG}_c2_pmc.json default-1920x1080-d5-exact-f32-n1 20 20 > gpurun_out/${TAG}_c2_pmc.txt || exit 1
+  grep -E "window_ns|f64_issue|wait_any_share|hbm_bytes" gpurun_out/${TAG}_c2_pmc.txt ;;
+prof5)
+  bash scripts/profile.sh prof_${TAG}_c5 $C5 --steps 6 --warmup 3 --iso 4 > gpurun_out/prof_${TAG}_c5.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_c5.log; exit 1; }
+  python3 scripts/pmc_summary.py gpurun_out/prof_${TAG}_c5 gpurun_out/${TAG}_c5_pmc.json s256-4096x4096-d8-exact-f32-n1-spp16 6 4 16 > gpurun_out/${TAG}_c5_pmc.txt || exit 1
+  grep -E "window_ns|f64_issue|wait_any_share|hbm_bytes" gpurun_out/${TAG}_c5_pmc.txt ;;
+esac

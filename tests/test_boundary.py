@@ -45,7 +45,7 @@ def test_library_targets_gfx950(tmp_path):
 
 def test_abi_version_and_errors(native):
     L = native.lib()
-    assert L.rt_abi_version() == 4
+    assert L.rt_abi_version() == 5
     for code in (N.RT_OK, N.RT_DONE, N.RT_EBADARG, N.RT_ENODEV, N.RT_EHIP, N.RT_ENOMEM, N.RT_ETOOBIG):
         assert N.strerror(code) and N.strerror(code) != "unknown error"
     assert N.strerror(-99) == "unknown error"
@@ -99,6 +99,47 @@ def test_scene_canon_bitwise_rule(native):
         e.canon = -1
     assert L.rt_scene_canon(el, len(el)) == N.RT_OK
     assert el[len(s) - 1].canon == 3 and el[3].canon == 3 and el[4].canon == 4
+
+
+def test_no_count_limits(native):
+    """Scenes of any size validate (the reference scans any list and folds over every light,
+    raytracer.erl:300-346, :209-252): 5,000 spheres, 100 lights."""
+    L = native.lib()
+    for sc in (scenes.named("s5000"), scenes.named("s64l100"), scenes.synthetic_scene(16, 7, n_lights=300)):
+        el = N.marshal(sc)
+        assert L.rt_scene_check(el, len(el)) == N.RT_OK
+
+
+def test_scene_canon_large_matches_prefix_rule(native):
+    """rt_scene_canon (hashed) against the definition — the first earlier self-canonical element of
+    the same kind with the same payload bytes — on a 3,000-element list with planted duplicates
+    (some with caller-given canon values)."""
+    import random
+    L = native.lib()
+    base = scenes.synthetic_scene(1500, 11, n_lights=8)
+    rnd = random.Random(5)
+    sc = list(base)
+    for _ in range(1500):
+        sc.insert(rnd.randrange(1, len(sc) + 1), base[rnd.randrange(1, len(base))])
+    el = N.marshal(sc)
+    want = []
+    for i in range(len(el)):
+        el[i].canon = -1 if rnd.random() < 0.9 else i  # a few elements claim to be their own class
+    given = [e.canon for e in el]
+    nb = {N.RT_CAMERA: 72, N.RT_POINT_LIGHT: 72, N.RT_SPHERE: 80, N.RT_TRIANGLE: 120, N.RT_PLANE: 80}
+    raw = [bytes(e.u)[:nb.get(e.kind, 0)] for e in el]
+    for i in range(len(el)):
+        c = given[i]
+        if c < 0:
+            c = i
+            if nb.get(el[i].kind, 0):
+                for j in range(i):
+                    if el[j].kind == el[i].kind and want[j] == j and raw[j] == raw[i]:
+                        c = j
+                        break
+        want.append(c)
+    assert L.rt_scene_canon(el, len(el)) == N.RT_OK
+    assert [e.canon for e in el] == want
 
 
 def test_marshal_badarg():

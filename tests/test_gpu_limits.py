@@ -1,0 +1,103 @@
+"""Inputs the reference renders at any size: recursion depth, lights and objects.
+
+The reference has no limits: pixel_colour_from_ray/3 recurses to any depth (raytracer.erl:186-203),
+lighting_function/6 folds over every light (:209-252) and nearest_object_intersecting_ray/6 scans any
+list (:300-346).  The library renders every such input (only RT_ENOMEM remains): the wavefront
+engine's per-level queues, events and counters are sized per frame; scenes over the occluder-mask
+budget (OCC_MAX_TESTS) shade their shadow rays through shadow cones; the sphere BVH's stack holds
+trees of up to 65,536 spheres.  Each case is checked against the C oracle (memoised mode: brute-force
+scans, reflection-chain levels identical, |delta| <= 1e-5) and, bit for bit, against the brute-force
+scans (RT_CFG_CULL = 0) through the bench's own path.
+"""
+import numpy as np
+import pytest
+
+from eraytracer_amd import _native as N
+from eraytracer_amd import records, scenes
+from eraytracer_amd.raytracer import render
+from tests.test_gpu_frames import bench_frames, nonbitwise
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _one_light_default():
+    """The default scene (raytracer.erl:618-665) without its second light: the reference's
+    recursion then costs one call per level, so deep frames are what BEAM itself renders."""
+    sc = records.scene()
+    lights = [i for i, t in enumerate(sc) if t[0] == "point_light"]
+    return [t for i, t in enumerate(sc) if i not in lights[1:]]
+
+
+def _check_rows(oracle, scene, w, h, d, rows, img, lv):
+    el = N.marshal(scene)
+    for r in rows:
+        ref, rlv = oracle.render(el, w, h, d, mode=oracle.MEMO, row0=r, nrows=1, levels=True)
+        np.testing.assert_array_equal(lv[r:r + 1], rlv, err_msg=f"row {r}: reflection chains differ")
+        err = float(np.abs(img[r:r + 1] - ref).max())
+        assert err <= TOL, f"row {r}: max |delta| {err}"
+
+
+@pytest.mark.parametrize("d", [17, 24, 40, 300])
+def test_depth_beyond_sixteen_whole_frame(oracle, d):
+    """The default scene with one light at depth 17 / 24 / 40 / 300 (160x120, whole frame; 1,365 of
+    its pixels reflect to the full depth, and at 300 their level counts saturate at 255): levels and
+    colours against the oracle; the levels render (side-stream kernels, one event pair per level)
+    equals the bench path (k_reflect_shade + inline walks), which equals its brute-force frame."""
+    scene = _one_light_default()
+    img, lv = render(160, 120, scene, d, levels=True)
+    ref, rlv = oracle.render(N.marshal(scene), 160, 120, d, mode=oracle.MEMO, levels=True)
+    np.testing.assert_array_equal(lv, rlv)
+    assert float(np.abs(img - ref).max()) <= TOL
+    print(f"depth {d}: deepest chain {int(lv.max())} levels, {int((lv > 16).sum())} pixels deeper than 16")
+    fast = bench_frames(scene, 160, 120, d)
+    brute = bench_frames(scene, 160, 120, d, cull=False)
+    assert nonbitwise(fast, img) == 0
+    assert nonbitwise(fast, brute) == 0
+    # the forward-order engine (fused kernel, no per-level LDS) at the same depth
+    fo = render(160, 120, scene, d, order="fast")
+    assert float(np.abs(fo - ref).max()) <= TOL
+
+
+def test_deep_chains_exist_at_depth_24(oracle):
+    """Depth 24 is not vacuous: the default scene's triangle reflections (negative t wins,
+    raytracer.erl:436-452) keep some chains alive past level 16."""
+    scene = _one_light_default()
+    _, rlv = oracle.render(N.marshal(scene), 160, 120, 24, mode=oracle.MEMO, levels=True)
+    _, lv = render(160, 120, scene, 24, levels=True)
+    np.testing.assert_array_equal(lv, rlv)
+    assert int(rlv.max()) > 16, f"deepest chain {int(rlv.max())}"
+
+
+def test_hundred_lights_rows_and_brute_force(oracle):
+    """S64 with 100 point lights (no 32-light shadow words: the walks re-test the shadows), 256x192
+    depth 5: sampled rows against the oracle, the whole frame bitwise against brute force; and the
+    default scene's objects with 70 lights (the fused engine) against the oracle."""
+    scene = scenes.named("s64l100")
+    w, h, d = 256, 192, 5
+    img, lv = render(w, h, scene, d, levels=True)
+    _check_rows(oracle, scene, w, h, d, (0, 47, 96, 140, 191), img, lv)
+    fast = bench_frames(scene, w, h, d)
+    assert nonbitwise(fast, img) == 0
+    assert nonbitwise(fast, bench_frames(scene, w, h, d, cull=False)) == 0
+    base = records.scene()
+    lights = scenes.synthetic_scene(1, 0x11, n_lights=70)[1:71]
+    mixed = base[:1] + lights + [t for t in base[1:] if t[0] != "point_light"]
+    img2, lv2 = render(96, 72, mixed, 4, levels=True)
+    ref2, rlv2 = oracle.render(N.marshal(mixed), 96, 72, 4, mode=oracle.MEMO, levels=True)
+    np.testing.assert_array_equal(lv2, rlv2)
+    assert float(np.abs(img2 - ref2).max()) <= TOL
+
+
+@pytest.mark.parametrize("name", ["s2000", "s5000"])
+def test_thousands_of_spheres_rows_and_brute_force(oracle, name):
+    """S2000 (occluder masks at the budget's edge, 16 cells over 32 chunks, BVH depth 13) and S5000
+    (over the budget: shadow cones; BVH depth 15, more than the old 12-entry stack) at depth 5,
+    256x192: sampled rows against the oracle, the whole frame bitwise against brute force."""
+    scene = scenes.named(name)
+    w, h, d = 256, 192, 5
+    img, lv = render(w, h, scene, d, levels=True)
+    _check_rows(oracle, scene, w, h, d, (0, 95, 191), img, lv)
+    fast = bench_frames(scene, w, h, d)
+    assert nonbitwise(fast, img) == 0
+    assert nonbitwise(fast, bench_frames(scene, w, h, d, cull=False)) == 0
