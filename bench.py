@@ -36,12 +36,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# Hardware queues per process (HIP's default, and the GPU box's setting, is 4): frames in
-# flight each use a stream of their own, and with RCCL's streams beside them 4 queues would be
-# shared behind event waits (measured: S64 4096^2 d5, 4 frames in flight, 0.68 ms per frame
-# with 4 queues, 0.61 with 8).  Set before the HIP runtime initialises.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# Hardware queues per process (--hw-queues; HIP's default, and the GPU box's setting, is 4): frames
+# in flight each use a stream of their own, and with RCCL's streams beside them 4 queues are shared
+# behind event waits.  bench.py raises it to 8 unless told otherwise (a library caller such as a NIF
+# process keeps HIP's 4: DESIGN.md §6 has the line at 4 beside this one).  Set in main() before the
+# HIP runtime initialises.
+DEFAULT_HW_QUEUES = 8
 
 PEAK_FP64_VALU_TOPS = 39.3   # MI355X FP64 vector 78.6 TFLOP/s counting an FMA as 2 (spec); this path has no FMA
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
@@ -77,9 +77,24 @@ def parse():
     ap.add_argument("--priorities", default="auto",
                     help="comma-separated stream priority per in-flight slot (torch: lower = higher priority; "
                          "auto: FrameRenderer's default, half the slots high with >= 4 in flight and spp 1; none)")
+    ap.add_argument("--hw-queues", type=int, default=DEFAULT_HW_QUEUES,
+                    help="GPU_MAX_HW_QUEUES for this process (default 8; 0 = leave the environment's, HIP's default 4)")
+    ap.add_argument("--no-setup", action="store_true",
+                    help="skip the setup-cost leg (scene compile, primary masks, new-scene and cold frames)")
     ap.add_argument("--gather", default="compact", choices=["compact", "dense"],
                     help="N > 1: compact = background pixels not sent (rt_slab_pack, default); dense = whole slabs")
     return ap.parse_args()
+
+
+def parse_priorities(text: str):
+    """--priorities "0,-1,...": one HIP stream priority (0 or -1) per frame in flight."""
+    try:
+        pr = [int(x) for x in text.split(",")]
+    except ValueError:
+        raise SystemExit(f"--priorities: comma-separated 0 / -1 values, 'auto' or 'none'; got {text!r}")
+    if any(p not in (0, -1) for p in pr):
+        raise SystemExit(f"--priorities: each value must be 0 or -1 (HIP's two stream priorities); got {text!r}")
+    return pr
 
 
 def free_port() -> int:
@@ -193,8 +208,8 @@ DOMINANT = {"wave": ("k_reflect_shade#0", "RT_KT_LEVEL1",
 
 
 def engine_of(N, fr, spp):
-    """The engine rt_launch runs for this context (rt_engine: the library's own decision,
-    RT_ENGINE / RT_FUSED_MAX_OBJECTS included)."""
+    """The engine rt_launch runs for this context (rt_engine: the library's own decision — the
+    RT_ENGINE environment override, else the compile-time FUSED_MAX_OBJECTS crossover)."""
     e = N.check(N.lib().rt_engine(fr._ps[0], spp), "rt_engine")
     return "fused" if e == N.RT_ENGINE_FUSED else "wave"
 
@@ -206,6 +221,10 @@ def f64_insts(c):
 
 def main():
     args = parse()
+    if not 0 <= args.hw_queues <= 32:
+        sys.exit("bench.py: --hw-queues must be in 0..32")
+    if args.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # python3 bench.py --gpus N: start the N ranks ourselves (nothing has touched HIP yet)
         sys.exit(self_launch(sys.argv[1:], args.gpus))
@@ -238,7 +257,7 @@ def main():
     fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
                        precision=args.precision, order=args.order, spp=args.spp, seed=args.seed, inflight=inflight,
                        priorities=("auto" if args.priorities == "auto" else None if args.priorities == "none" else
-                                   [int(x) for x in args.priorities.split(",")]))
+                                   parse_priorities(args.priorities)))
 
     # untimed: work count of this rank's rows (levels of every pixel's reflection chain)
     lv_fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
@@ -435,6 +454,7 @@ def main():
                        "stream_priorities": [st.priority for st in fr.streams] if fr.streams else None,
                        "parallelism": f"rows{world}" + (f"+rccl_{args.gather}_gather" if world > 1 else ""),
                        "world_size": world, "rccl_ranks": dist.get_world_size() if world > 1 else 1,
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4),
                        "spheres": counts["spheres"], "triangles": counts["triangles"], "planes": counts["planes"],
                        "lights": counts["lights"]},
             "roofline": roof,
@@ -452,6 +472,8 @@ def main():
         }
         if checked is not None:
             line["self_check"] = checked
+        if world == 1 and not args.no_setup:
+            line["setup"] = setup_costs(N, scene, W, H, args, fr)
         if world == 1 and not args.no_boundary:
             line.update(boundary_legs(N, scene, W, H, args))
         if world == 1 and not args.no_cpu_baseline:
@@ -513,6 +535,122 @@ def self_check(fr, pipe, scene, args, rank, world, local):
     torch.cuda.synchronize()
     return {"frames": n, "equal_bitwise": True, "what": "compact-gathered frames == one-shard rt_launch frames"} \
         if rank == 0 else None
+
+
+def setup_costs(N, scene, W, H, args, fr):
+    """What the headline amortises (it renders one fixed scene and camera, prepared before the timed
+    region): the reference's unit of work is one cold raytrace/5 call (raytracer.erl:695-705,
+    :723-733).  All figures in milliseconds:
+      compile_ms             rt_prepare: host compile_scene (tables, occluder masks, BVH) + upload, a fresh
+                             context each time (median of 5, host wall clock)
+      pmask_ms               k_pmask, the primary rays' candidate masks of a new (scene, camera, frame
+                             geometry) on a fresh context (HIP events on its stream; 0 when the engine has none)
+      first_frame_ms         that context's first frame: work-space allocation + k_pmask + the frame (wall)
+      single_frame_kernel_ms one frame, nothing else in flight, on a warm context (median of 10, HIP events)
+      new_scene_frame_ms     rt_update_scene with one sphere moved + the frame, on a warm context, to the
+                             end of the frame (host wall clock, mean of 20 steps; scene_update_ms: the update alone)
+      cold_*                 a child process started before any GPU call: hip_init_ms (runtime and device
+                             initialisation), cold_boundary_ms (its first rt_render: context, compile, upload,
+                             work space, masks, frame, copy to pageable host memory; C-side total_ms) and
+                             warm_boundary_ms (its second, identical call)"""
+    import ctypes
+    import statistics
+
+    import torch
+    L = N.lib()
+    el = N.marshal(scene)
+    dev = torch.cuda.current_device()
+    out = {}
+    ts, p = [], None
+    for i in range(5):
+        q = ctypes.c_void_p()
+        t0 = time.perf_counter()
+        N.check(L.rt_prepare(el, len(el), dev, ctypes.byref(q)), "rt_prepare")
+        ts.append((time.perf_counter() - t0) * 1e3)
+        if p is not None:
+            L.rt_release(p)
+        p = q
+    out["compile_ms"] = round(statistics.median(ts), 3)
+    st = torch.cuda.Stream()
+    slab = torch.empty((H, W, 3), dtype=fr.dtype, device="cuda")
+    prec, order = fr.prec, fr.order
+
+    def frame(p_):
+        N.check(L.rt_launch_spp(p_, W, H, args.depth, args.row_block, 0, 1, prec, order, args.spp, args.seed,
+                                slab.data_ptr(), None, st.cuda_stream), "rt_launch_spp")
+    try:
+        N.check(L.rt_configure(p, N.RT_CFG_SIDE_STREAMS, 0), "rt_configure")
+        N.check(L.rt_configure(p, N.RT_CFG_KERNEL_TIMING, N.RT_KT_PMASK), "rt_configure")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        frame(p)
+        st.synchronize()
+        out["first_frame_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+        ms, n = ctypes.c_double(0), ctypes.c_uint64(0)
+        N.check(L.rt_kernel_time(p, N.RT_KT_PMASK, ctypes.byref(ms), ctypes.byref(n), 1), "rt_kernel_time")
+        out["pmask_ms"] = round(ms.value / n.value, 4) if n.value else 0.0
+        N.check(L.rt_configure(p, N.RT_CFG_KERNEL_TIMING, 0), "rt_configure")
+        ks = []
+        for _ in range(10):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            frame(p)
+            e1.record(st)
+            st.synchronize()
+            ks.append(e0.elapsed_time(e1))
+        out["single_frame_kernel_ms"] = round(statistics.median(ks), 4)
+        sph = [i for i in range(len(el)) if el[i].kind == N.RT_SPHERE]
+        if sph:
+            k = sph[0]
+            x0 = el[k].u.sphere.center.x
+            tu, tf = [], []
+            for s in range(20):
+                el[k].u.sphere.center.x = x0 + (s + 1) * 2.0 ** -10  # one sphere moved per step
+                el[k].canon = -1
+                st.synchronize()
+                t0 = time.perf_counter()
+                N.check(L.rt_update_scene(p, el, len(el)), "rt_update_scene")
+                t1 = time.perf_counter()
+                frame(p)
+                st.synchronize()
+                t2 = time.perf_counter()
+                tu.append((t1 - t0) * 1e3)
+                tf.append((t2 - t0) * 1e3)
+            out["new_scene_frame_ms"] = round(statistics.mean(tf), 3)
+            out["scene_update_ms"] = round(statistics.mean(tu), 3)
+    finally:
+        L.rt_release(p)
+    out.update(cold_boundary(W, H, args))
+    out["note"] = ("the headline renders one scene and camera prepared before the timed region: it excludes "
+                   "compile_ms and pmask_ms (paid once per scene / frame geometry) and overlaps frames "
+                   "(single_frame_kernel_ms is a frame alone); see setup_costs() in bench.py")
+    return out
+
+
+def cold_boundary(W, H, args):
+    """The first rt_render of a process (a child started before any GPU call; see setup_costs)."""
+    code = (
+        "import json, sys, time\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "from eraytracer_amd import _native as N, scenes\n"
+        "from eraytracer_amd.raytracer import render\n"
+        f"sc = scenes.named({args.scene!r})\n"
+        "import ctypes\n"
+        "t0 = time.perf_counter(); n = ctypes.c_int(0); N.lib().rt_device_count(ctypes.byref(n))\n"
+        "hip = (time.perf_counter() - t0) * 1e3\n"
+        "r = {'hip_init_ms': round(hip, 3)}\n"
+        "for k in ('cold_boundary_ms', 'warm_boundary_ms'):\n"
+        "    st = {}\n"
+        f"    render({W}, {H}, sc, {args.depth}, precision={args.precision!r}, order={args.order!r}, stats=st, "
+        f"spp={args.spp}, seed={args.seed})\n"
+        "    r[k] = round(st['total_ms'], 3)\n"
+        "print(json.dumps(r))\n")
+    try:
+        res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+        return json.loads(res.stdout.strip().splitlines()[-1]) if res.returncode == 0 else {
+            "cold_error": (res.stderr or res.stdout)[-300:]}
+    except Exception as e:  # the setup leg is a report: a failure is recorded, not fatal
+        return {"cold_error": repr(e)[-300:]}
 
 
 def boundary_legs(N, scene, W, H, args):

@@ -28,7 +28,7 @@ RT_MAX_SHARDS = 64
 RT_CFG_SIDE_STREAMS = 1
 RT_CFG_KERNEL_TIMING = 2
 RT_CFG_CULL = 3
-RT_KT_PRIMARY, RT_KT_LEVEL1, RT_KT_RENDER = 1, 2, 4
+RT_KT_PRIMARY, RT_KT_LEVEL1, RT_KT_RENDER, RT_KT_PMASK = 1, 2, 4, 8
 RT_LEVELS_HIT = 1
 RT_ENGINE_WAVE, RT_ENGINE_FUSED = 0, 1
 
@@ -36,6 +36,7 @@ RT_ENGINE_WAVE, RT_ENGINE_FUSED = 0, 1
 EXPORTS = (
     "rt_abi_version", "rt_strerror", "rt_device_count", "rt_scene_check", "rt_scene_canon",
     "rt_render", "rt_prepare", "rt_shard_rows", "rt_launch", "rt_launch_spp", "rt_unshard", "rt_configure", "rt_release",
+    "rt_update_scene",
     "rt_ppm_bound", "rt_ppm_format", "rt_render_ppm_file",
     "rt_slab_header_bytes", "rt_slab_pack", "rt_slab_unpack", "rt_selftest_math",
     "rt_host_alloc", "rt_host_free", "rt_reset_contexts", "rt_kernel_time", "rt_engine",
@@ -138,6 +139,7 @@ def lib() -> ctypes.CDLL:
     L.rt_render_ppm_file.argtypes = [vp, u32, u32, u32, u32, vp, u32, ctypes.c_char_p, vp]
     L.rt_unshard.argtypes = [vp, u32, u32, u32, u32, i32, vp, vp]
     L.rt_release.argtypes = [vp]
+    L.rt_update_scene.argtypes = [vp, ctypes.POINTER(RtElem), u32]
     L.rt_configure.argtypes = [vp, i32, ctypes.c_int64]
     L.rt_engine.argtypes = [vp, u32]
     L.rt_selftest_math.argtypes = [i32, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]

@@ -1626,7 +1626,7 @@ struct rt_prepared {
         size_t head = 0, n = 0;
         double sum_ms = 0;
         unsigned long long count = 0;
-    } kt[3];
+    } kt[4];
     hipStream_t cap = nullptr;
     hipGraphExec_t gexec = nullptr;
     long long gkey[12] = {};
@@ -1673,7 +1673,9 @@ void apply_cull(rt_prepared *p) {
 }
 
 constexpr size_t KT_RING = 64;
-int kt_index(int kernel) { return kernel == RT_KT_PRIMARY ? 0 : kernel == RT_KT_LEVEL1 ? 1 : kernel == RT_KT_RENDER ? 2 : -1; }
+int kt_index(int kernel) {
+    return kernel == RT_KT_PRIMARY ? 0 : kernel == RT_KT_LEVEL1 ? 1 : kernel == RT_KT_RENDER ? 2 : kernel == RT_KT_PMASK ? 3 : -1;
+}
 void kt_fold_oldest(rt_prepared::KTimer &t) {
     const size_t i = (t.head + KT_RING - t.n) % KT_RING;
     float ms = 0;
@@ -1874,6 +1876,10 @@ int rt_prepare_scene(rt_prepared *p, const rt_elem *scene, uint32_t n) {
 
 extern "C" {
 
+int rt_update_scene(rt_prepared *p, const rt_elem *scene, uint32_t n_elems) {
+    return rt_prepare_scene(p, scene, n_elems);
+}
+
 int rt_configure(rt_prepared *p, int option, int64_t value) {
     if (!p) return RT_EBADARG;
     switch (option) {
@@ -1882,7 +1888,7 @@ int rt_configure(rt_prepared *p, int option, int64_t value) {
         p->side_mode = (int)value;
         return RT_OK;
     case RT_CFG_KERNEL_TIMING:
-        if (value < 0 || value > 7) return RT_EBADARG;
+        if (value < 0 || value > 15) return RT_EBADARG;
         p->timing_mask = (int)value;
         return RT_OK;
     case RT_CFG_CULL:
@@ -2105,6 +2111,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
                 RT_OK)
                 return rc;
             const dim3 pg((unsigned)std::min<size_t>(4096, (nhalf + 3) / 4));
+            KtScope kt(p, RT_KT_PMASK, st);
             if (spp > 1)
                 hipLaunchKernelGGL(k_pmask<true>, pg, dim3(256), 0, st, p->hdr, p->d_tab, p->d_itab, W, H, rb, sh, ns,
                                    slab_all, (int)nhalf, p->d_pmask);
@@ -2248,8 +2255,7 @@ int launch_wavefront(rt_prepared *p, int W, int H, int D, int rb, int sh, int ns
     } while (0)
                 // levels traversing the sphere BVH (unstaged scenes only): the BVH instantiations
                 const bool bvh_k = bvh_at(k);
-                if (staged && bvh_k) RT_RS(2, true, lds_r(k), true);
-                else if (staged && k == 1) RT_RS(2, false, lds, false);
+                if (staged && k == 1) RT_RS(2, false, lds, false); // (staged: never the BVH, bvh_at)
                 else if (staged) RT_RS(2, true, lds, false);
                 else if (sph_only && bvh_k) RT_RS(1, true, lds_r(k), true);
                 else if (sph_only && k == 1) RT_RS(1, false, lds, false);

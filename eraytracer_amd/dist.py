@@ -383,6 +383,9 @@ class FrameRenderer:
             priorities = [-1] * (inflight // 2) + [0] * (inflight - inflight // 2) \
                 if inflight >= 4 and spp == 1 else None
         pr = list(priorities) if priorities is not None else [0] * inflight
+        if not pr or len(pr) > inflight or any(p not in (0, -1) for p in pr):
+            raise ValueError(f"priorities: 1 to {inflight} values, each 0 or -1 (HIP's two stream priorities), "
+                             f"got {pr!r}; a shorter list is repeated over the frames in flight")
         self.streams = [torch.cuda.Stream(self.device, priority=pr[i % len(pr)]) for i in range(inflight)] \
             if inflight > 1 else None
         self.stream = torch.cuda.current_stream(self.device)
@@ -422,7 +425,7 @@ class FrameRenderer:
         stream each runs on (every slot context); 0 stops."""
         for p in self._ps:
             N.check(self.L.rt_configure(p, N.RT_CFG_KERNEL_TIMING, mask), "rt_configure")
-            for k in (N.RT_KT_PRIMARY, N.RT_KT_LEVEL1, N.RT_KT_RENDER):
+            for k in (N.RT_KT_PRIMARY, N.RT_KT_LEVEL1, N.RT_KT_RENDER, N.RT_KT_PMASK):
                 N.check(self.L.rt_kernel_time(p, k, None, None, 1), "rt_kernel_time")  # reset
 
     def kernel_time(self, kernel: int):

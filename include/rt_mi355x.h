@@ -232,6 +232,10 @@ int rt_launch_spp(rt_prepared *p, uint32_t width, uint32_t height, uint32_t dept
 int rt_unshard(const void *d_slabs, uint32_t width, uint32_t height, uint32_t row_block,
                uint32_t nshards, int precision, void *d_image, void *stream);
 int rt_release(rt_prepared *p);
+/* Replace the scene of a prepared context in place (an animated scene: the next rt_launch renders
+ * the new one): the scene is compiled and uploaded as by rt_prepare, the context's work space,
+ * streams and options are kept.  No launch of p may be in flight (synchronise its stream first). */
+int rt_update_scene(rt_prepared *p, const rt_elem *scene, uint32_t n_elems);
 /* Per-context launch options.
  * RT_CFG_SIDE_STREAMS: 1 = a frame's shading runs on two low-priority side streams of the
  *   context beside its reflection chain (the fastest for ONE frame in flight); 0 = every
@@ -248,6 +252,8 @@ int rt_release(rt_prepared *p);
 #define RT_KT_LEVEL1 2   /* the level-0 shading + level-1 reflection pass (k_reflect_shade(1); with
                             side streams or levels: k_reflect(1)) */
 #define RT_KT_RENDER 4   /* k_render: the fused engine's one kernel per frame */
+#define RT_KT_PMASK 8    /* k_pmask: the primary rays' candidate masks, computed when the scene, the culling
+                            mode or the frame geometry changes (the wavefront engine, culled scenes) */
 /* RT_CFG_CULL: 1 = the default: scans skip objects a conservative filter proves cannot be hit
  *   (wave beams and shadow cones, per-light occluder masks, the sphere BVH); 0 = brute force,
  *   every nearest scan and every shadow test visits every object of the scene, as the

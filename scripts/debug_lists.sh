@@ -18,5 +18,6 @@ else
     "tests/test_gpu_frames.py::test_fused_path_with_row_passes" \
     "tests/test_gpu_fullsize.py::test_bvh_forced_on_every_level_and_scene" \
     "tests/test_gpu_fullsize.py::test_config5_rows_through_the_bvh_path" \
-    "tests/test_gpu_fullsize.py::test_inline_walks_dense_deep_levels"
+    "tests/test_gpu_fullsize.py::test_inline_walks_dense_deep_levels" \
+    "tests/test_gpu_limits.py"
 fi

@@ -4,6 +4,7 @@
 #   bash scripts/gpu_r06.sh TAG test      GPU parity suite, then the RT_DEBUG_LISTS build's wavefront tests
 #   bash scripts/gpu_r06.sh TAG bench     bench lines: config 3 (driver-style 20/5 and default), configs 2, 5
 #   bash scripts/gpu_r06.sh TAG c3        config 3 driver-style bench line only
+#   bash scripts/gpu_r06.sh TAG setup     config 3 lines with the setup leg (8 and 4 HW queues), config 5's, the N = 8 floor
 #   bash scripts/gpu_r06.sh TAG prof3     rocprofv3 kernel trace + PMC passes of config 3
 #   bash scripts/gpu_r06.sh TAG prof5     the same for config 5 (prof2: config 2)
 set -o pipefail
@@ -27,6 +28,13 @@ test)
   tail -1 gpurun_out/debug_lists_$TAG.log ;;
 c3)
   b c3d --steps 20 --warmup 5 --no-boundary --no-cpu-baseline || exit 1 ;;
+setup)
+  b c3d --steps 20 --warmup 5 --no-boundary --no-cpu-baseline || exit 1
+  b c3d_q4 --steps 20 --warmup 5 --no-boundary --no-cpu-baseline --hw-queues 0 --no-setup || exit 1
+  b c5s $C5 --steps 6 --warmup 3 --no-boundary --no-cpu-baseline || exit 1
+  timeout -k 10 300 python scripts/n8_floor.py > gpurun_out/${TAG}_n8_floor.json 2> gpurun_out/${TAG}_n8_floor.err || { tail -5 gpurun_out/${TAG}_n8_floor.err; exit 1; }
+  cat gpurun_out/${TAG}_n8_floor.json
+  python3 -c "import json,sys; [print(n, json.dumps(json.load(open(f'gpurun_out/${TAG}_bench_'+n+'.json')).get('setup'))) for n in ('c3d','c5s')]" ;;
 bench)
   make -C oracle > /dev/null || exit 1
   timeout -k 10 200 python scripts/cpu_config1.py > gpurun_out/${TAG}_cfg1.json && cat gpurun_out/${TAG}_cfg1.json || exit 1

@@ -52,3 +52,24 @@ def test_main_inside_torchrun_does_not_relaunch(monkeypatch):
     with pytest.raises(SystemExit) as e:
         bench.main()
     assert "WORLD_SIZE=2" in str(e.value.code)
+
+
+@pytest.mark.parametrize("flag,want", [([], "8"), (["--hw-queues", "0"], "4"), (["--hw-queues", "4"], "4"),
+                                       (["--hw-queues", "16"], "16")])
+def test_hw_queues_flag(monkeypatch, flag, want):
+    """--hw-queues sets GPU_MAX_HW_QUEUES before anything touches HIP (default 8; 0 keeps the
+    environment's value, here the box's 4)."""
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    monkeypatch.setenv("WORLD_SIZE", "2")  # stops main() at the WORLD_SIZE check, before any GPU work
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "1"] + flag)
+    with pytest.raises(SystemExit):
+        bench.main()
+    import os
+    assert os.environ["GPU_MAX_HW_QUEUES"] == want
+
+
+def test_priorities_parser():
+    assert bench.parse_priorities("0,-1,0") == [0, -1, 0]
+    for bad in ("", "1", "0,x", "-2"):
+        with pytest.raises(SystemExit):
+            bench.parse_priorities(bad)
