@@ -36,12 +36,13 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# Hardware queues per process (--hw-queues; HIP's default, and the GPU box's setting, is 4): frames
-# in flight each use a stream of their own, and with RCCL's streams beside them 4 queues are shared
-# behind event waits.  bench.py raises it to 8 unless told otherwise (a library caller such as a NIF
-# process keeps HIP's 4: DESIGN.md §6 has the line at 4 beside this one).  Set in main() before the
-# HIP runtime initialises.
-DEFAULT_HW_QUEUES = 8
+# Hardware queues per process (--hw-queues; HIP's default, and the GPU box's setting, is 4).  At
+# N = 1 the bench keeps the environment's value, as a library caller (a NIF process) does: 4 and 8
+# queues measured the same (profiles/r06c_bench_c3d.json 0.3935 ms at 8, r06c_bench_c3d_q4.json
+# 0.3908 at 4).  With N > 1 ranks RCCL's streams and the exchange's side stream join the frames' streams,
+# and 4 queues would be shared behind event waits: 8 there.  Set in main() before the HIP runtime
+# initialises.
+DEFAULT_HW_QUEUES_MULTI = 8
 
 PEAK_FP64_VALU_TOPS = 39.3   # MI355X FP64 vector 78.6 TFLOP/s counting an FMA as 2 (spec); this path has no FMA
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
@@ -77,8 +78,9 @@ def parse():
     ap.add_argument("--priorities", default="auto",
                     help="comma-separated stream priority per in-flight slot (torch: lower = higher priority; "
                          "auto: FrameRenderer's default, half the slots high with >= 4 in flight and spp 1; none)")
-    ap.add_argument("--hw-queues", type=int, default=DEFAULT_HW_QUEUES,
-                    help="GPU_MAX_HW_QUEUES for this process (default 8; 0 = leave the environment's, HIP's default 4)")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (0 = leave the environment's, HIP's default 4; "
+                         "default: 0 at --gpus 1, 8 with more)")
     ap.add_argument("--no-setup", action="store_true",
                     help="skip the setup-cost leg (scene compile, primary masks, new-scene and cold frames)")
     ap.add_argument("--gather", default="compact", choices=["compact", "dense"],
@@ -221,6 +223,8 @@ def f64_insts(c):
 
 def main():
     args = parse()
+    if args.hw_queues is None:
+        args.hw_queues = 0 if args.gpus == 1 else DEFAULT_HW_QUEUES_MULTI
     if not 0 <= args.hw_queues <= 32:
         sys.exit("bench.py: --hw-queues must be in 0..32")
     if args.hw_queues:

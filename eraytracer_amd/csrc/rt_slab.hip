@@ -136,6 +136,7 @@ __global__ __launch_bounds__(SLAB_BLOCK) void k_compact(const T *__restrict__ sl
     if (p >= px) return;
     if (!((mask[p / 64] >> (p % 64)) & 1ull)) return;
     const uint64_t r = rank_of(off, mask, p);
+    if (r >= px) return; // a consistent header never ranks past the slab (values hold px pixels)
     vals[r * 3] = slab[p * 3];
     vals[r * 3 + 1] = slab[p * 3 + 1];
     vals[r * 3 + 2] = slab[p * 3 + 2];
@@ -149,8 +150,8 @@ struct ShardPtrs {
 // one workgroup per (image row g, 256 columns): the row's shard and slab row are wave-uniform
 // (no per-lane division), each lane finds its pixel's mask bit and value
 template <typename T>
-__global__ __launch_bounds__(SLAB_BLOCK) void k_unpack(ShardPtrs sp, uint64_t mask_at, uint32_t W, uint32_t ncol,
-                                                       uint32_t rb, uint32_t ns, T *__restrict__ image) {
+__global__ __launch_bounds__(SLAB_BLOCK) void k_unpack(ShardPtrs sp, uint64_t mask_at, uint64_t px, uint32_t W,
+                                                       uint32_t ncol, uint32_t rb, uint32_t ns, T *__restrict__ image) {
     const uint32_t g = blockIdx.x / ncol, c = blockIdx.x - g * ncol;
     const uint32_t x = c * SLAB_BLOCK + threadIdx.x;
     if (x >= W) return;
@@ -161,8 +162,9 @@ __global__ __launch_bounds__(SLAB_BLOCK) void k_unpack(ShardPtrs sp, uint64_t ma
     const uint32_t *off = reinterpret_cast<const uint32_t *>(h + HDR_OFFS);
     const uint64_t *mask = reinterpret_cast<const uint64_t *>(h + mask_at);
     T c0 = 0, c1 = 0, c2 = 0;
-    if ((mask[p / 64] >> (p % 64)) & 1ull) {
-        const T *v = static_cast<const T *>(sp.vals[s]) + rank_of(off, mask, p) * 3;
+    const uint64_t r = ((mask[p / 64] >> (p % 64)) & 1ull) ? rank_of(off, mask, p) : px;
+    if (r < px) { // (a consistent header never ranks past the slab: values hold px pixels)
+        const T *v = static_cast<const T *>(sp.vals[s]) + r * 3;
         c0 = v[0];
         c1 = v[1];
         c2 = v[2];
@@ -240,10 +242,10 @@ int rt_slab_unpack(const void *const *d_headers, const void *const *d_values, ui
     const dim3 grid((unsigned)nblocks);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (precision == RT_OUT_F32)
-        hipLaunchKernelGGL(k_unpack<uint32_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, width, ncol, row_block,
+        hipLaunchKernelGGL(k_unpack<uint32_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, l.px, width, ncol, row_block,
                            nshards, static_cast<uint32_t *>(d_image));
     else
-        hipLaunchKernelGGL(k_unpack<uint64_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, width, ncol, row_block,
+        hipLaunchKernelGGL(k_unpack<uint64_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, l.px, width, ncol, row_block,
                            nshards, static_cast<uint64_t *>(d_image));
     SLABCHK(hipGetLastError());
     return RT_OK;

@@ -30,7 +30,7 @@ c3)
   b c3d --steps 20 --warmup 5 --no-boundary --no-cpu-baseline || exit 1 ;;
 setup)
   b c3d --steps 20 --warmup 5 --no-boundary --no-cpu-baseline || exit 1
-  b c3d_q4 --steps 20 --warmup 5 --no-boundary --no-cpu-baseline --hw-queues 0 --no-setup || exit 1
+  b c3d_q8 --steps 20 --warmup 5 --no-boundary --no-cpu-baseline --hw-queues 8 --no-setup || exit 1
   b c5s $C5 --steps 6 --warmup 3 --no-boundary --no-cpu-baseline || exit 1
   timeout -k 10 300 python scripts/n8_floor.py > gpurun_out/${TAG}_n8_floor.json 2> gpurun_out/${TAG}_n8_floor.err || { tail -5 gpurun_out/${TAG}_n8_floor.err; exit 1; }
   cat gpurun_out/${TAG}_n8_floor.json

@@ -75,19 +75,24 @@ def main():
         fr = FrameRenderer(scene, W, H, a.depth, rank=s, world=ns, precision="f32", inflight=3)
         fr_rows = fr.rows
         shard_ms.append(round(per_frame(fr), 4))
-        hdr = torch.empty(codec.header_bytes, dtype=torch.uint8, device="cuda")
-        val = torch.empty(fr.rows * W * 3, dtype=torch.float32, device="cuda")
+        # one header / values buffer per slot: packs of frames in flight must not share them (a
+        # header packed by two streams at once is inconsistent, as dist.CompactGather's ring avoids)
+        hdrs = [torch.empty(codec.header_bytes, dtype=torch.uint8, device="cuda") for _ in fr._ps]
+        vals = [torch.empty(fr.rows * W * 3, dtype=torch.float32, device="cuda") for _ in fr._ps]
 
-        def pack(i, fr=fr, hdr=hdr, val=val, s=s):
+        def pack(i, fr=fr, hdrs=hdrs, vals=vals, s=s):
+            j = (fr.n - 1) % len(fr._ps)  # the slot fr.launch() just used
             with torch.cuda.stream(fr.stream):
-                codec.pack(fr.slab, s, hdr, val)
+                codec.pack(fr.slab, s, hdrs[j], vals[j])
         shard_pack_ms.append(round(per_frame(fr, pack), 4))
         torch.cuda.synchronize()
+        hdr, val = hdrs[0], vals[0]
         cnt = int(hdr[:8].view(torch.int64).item())
         values_bytes.append(cnt * 3 * 4)
         headers.append(hdr.clone())
         values.append(val.clone())
         if s == 0:
+            pack_bufs = (hdrs, vals)
             # the pack alone (HIP events, back to back on one stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -115,8 +120,9 @@ def main():
     xs = torch.cuda.Stream()
 
     def pack_and_decode(i):
-        with torch.cuda.stream(fr0.stream):
-            codec.pack(fr0.slab, 0, headers[0], values[0])
+        j = (fr0.n - 1) % len(fr0._ps)
+        with torch.cuda.stream(fr0.stream):  # (its own slot's buffers; the decode reads the copies)
+            codec.pack(fr0.slab, 0, pack_bufs[0][j], pack_bufs[1][j])
         ev = torch.cuda.Event()
         ev.record(fr0.stream)
         xs.wait_event(ev)

@@ -5,7 +5,7 @@ TAG=${1:-prof}; shift || true
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="bench.py --steps 20 --warmup 10 --iso 20 --settle 0 --no-cpu-baseline --no-boundary $*"
+BENCH="bench.py --steps 20 --warmup 10 --iso 20 --settle 0 --no-cpu-baseline --no-boundary --no-setup $*"
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $BENCH > $OUT/trace.log 2>&1 || exit 1
 i=0

@@ -54,14 +54,14 @@ def test_main_inside_torchrun_does_not_relaunch(monkeypatch):
     assert "WORLD_SIZE=2" in str(e.value.code)
 
 
-@pytest.mark.parametrize("flag,want", [([], "8"), (["--hw-queues", "0"], "4"), (["--hw-queues", "4"], "4"),
-                                       (["--hw-queues", "16"], "16")])
-def test_hw_queues_flag(monkeypatch, flag, want):
-    """--hw-queues sets GPU_MAX_HW_QUEUES before anything touches HIP (default 8; 0 keeps the
-    environment's value, here the box's 4)."""
+@pytest.mark.parametrize("gpus,flag,want", [("1", [], "4"), ("2", [], "8"), ("1", ["--hw-queues", "0"], "4"),
+                                            ("1", ["--hw-queues", "8"], "8"), ("2", ["--hw-queues", "16"], "16")])
+def test_hw_queues_flag(monkeypatch, gpus, flag, want):
+    """--hw-queues sets GPU_MAX_HW_QUEUES before anything touches HIP (default: the environment's at
+    --gpus 1, 8 with more ranks; 0 keeps the environment's value, here the box's 4)."""
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
-    monkeypatch.setenv("WORLD_SIZE", "2")  # stops main() at the WORLD_SIZE check, before any GPU work
-    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "1"] + flag)
+    monkeypatch.setenv("WORLD_SIZE", "3")  # stops main() at the WORLD_SIZE check, before any GPU work
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", gpus] + flag)
     with pytest.raises(SystemExit):
         bench.main()
     import os
