@@ -175,6 +175,57 @@ __global__ __launch_bounds__(SLAB_BLOCK) void k_unpack(ShardPtrs sp, uint64_t ma
     o[2] = c2;
 }
 
+// Frames whose width is a multiple of 4: each thread decodes 4 consecutive pixels of an image row
+// (their mask bits share one word: p is a multiple of 4) and writes them as 16-byte stores (48 B of
+// binary32 RGB, 96 of binary64), one workgroup per (row, 1024 columns).  The frame is the bulk of
+// the decode's traffic (201 MB at 4096^2 f32 against ~55 MB of values for S64), so wide stores and a
+// quarter of the threads' rank computations are what its speed rests on (scripts/n8_floor.py).
+constexpr int UNPACK_PX = 4;
+template <typename T>
+__global__ __launch_bounds__(SLAB_BLOCK) void k_unpack4(ShardPtrs sp, uint64_t mask_at, uint64_t px, uint32_t W,
+                                                        uint32_t ncol, uint32_t rb, uint32_t ns, T *__restrict__ image) {
+    const uint32_t g = blockIdx.x / ncol, c = blockIdx.x - g * ncol;
+    const uint32_t x = (c * SLAB_BLOCK + threadIdx.x) * UNPACK_PX;
+    if (x >= W) return;
+    const uint32_t blk = g / rb, s = blk % ns;
+    const uint64_t lr = (uint64_t)(blk / ns) * rb + (g - blk * rb);
+    const uint64_t p = lr * W + x; // a multiple of 4 (W is)
+    const unsigned char *h = sp.hdr[s];
+    const uint32_t *off = reinterpret_cast<const uint32_t *>(h + HDR_OFFS);
+    const uint64_t *mask = reinterpret_cast<const uint64_t *>(h + mask_at);
+    const unsigned bits = (unsigned)(mask[p / 64] >> (p % 64)) & 0xFu;
+    T v[3 * UNPACK_PX];
+#pragma unroll
+    for (int k = 0; k < 3 * UNPACK_PX; ++k) v[k] = 0;
+    if (bits) {
+        uint64_t r = rank_of(off, mask, p);
+        if (r + __popc(bits) <= px) { // (a consistent header never ranks past the slab)
+            const T *src = static_cast<const T *>(sp.vals[s]);
+#pragma unroll
+            for (int k = 0; k < UNPACK_PX; ++k) {
+                if ((bits >> k) & 1u) {
+                    v[3 * k] = src[r * 3];
+                    v[3 * k + 1] = src[r * 3 + 1];
+                    v[3 * k + 2] = src[r * 3 + 2];
+                    ++r;
+                }
+            }
+        }
+    }
+    // 16-byte aligned: ((g * W + x) * 3 * sizeof(T)) is a multiple of 48 (x and W multiples of 4)
+    uint4 *o = reinterpret_cast<uint4 *>(image + ((uint64_t)g * W + x) * 3);
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            o[k] = make_uint4((unsigned)v[4 * k], (unsigned)v[4 * k + 1], (unsigned)v[4 * k + 2], (unsigned)v[4 * k + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            o[k] = make_uint4((unsigned)v[2 * k], (unsigned)(v[2 * k] >> 32), (unsigned)v[2 * k + 1],
+                              (unsigned)(v[2 * k + 1] >> 32));
+    }
+}
+
 bool args_ok(uint32_t width, uint32_t height, uint32_t row_block, uint32_t nshards, int precision) {
     if (width == 0 || height == 0 || row_block == 0 || nshards == 0 || nshards > RT_MAX_SHARDS) return false;
     if (precision != RT_OUT_F64 && precision != RT_OUT_F32) return false;
@@ -236,11 +287,24 @@ int rt_slab_unpack(const void *const *d_headers, const void *const *d_values, ui
         sp.hdr[s] = static_cast<const unsigned char *>(d_headers[s]);
         sp.vals[s] = d_values[s];
     }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (width % UNPACK_PX == 0) { // 4 pixels per thread, 16-byte stores
+        const uint32_t ncol = (width + SLAB_BLOCK * UNPACK_PX - 1) / (SLAB_BLOCK * UNPACK_PX);
+        const uint64_t nblocks = (uint64_t)ncol * height;
+        if (nblocks >= (1ull << 31)) return RT_ETOOBIG;
+        if (precision == RT_OUT_F32)
+            hipLaunchKernelGGL(k_unpack4<uint32_t>, dim3((unsigned)nblocks), dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, l.px,
+                               width, ncol, row_block, nshards, static_cast<uint32_t *>(d_image));
+        else
+            hipLaunchKernelGGL(k_unpack4<uint64_t>, dim3((unsigned)nblocks), dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, l.px,
+                               width, ncol, row_block, nshards, static_cast<uint64_t *>(d_image));
+        SLABCHK(hipGetLastError());
+        return RT_OK;
+    }
     const uint32_t ncol = (width + SLAB_BLOCK - 1) / SLAB_BLOCK;
     const uint64_t nblocks = (uint64_t)ncol * height;
     if (nblocks >= (1ull << 31)) return RT_ETOOBIG;
     const dim3 grid((unsigned)nblocks);
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (precision == RT_OUT_F32)
         hipLaunchKernelGGL(k_unpack<uint32_t>, grid, dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, l.px, width, ncol, row_block,
                            nshards, static_cast<uint32_t *>(d_image));

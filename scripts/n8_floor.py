@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--scene", default="s64")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--depth", type=int, default=5)
-    ap.add_argument("--reps", type=int, default=40)
+    ap.add_argument("--reps", type=int, default=100)
+    ap.add_argument("--inflight", type=int, default=3, help="frames in flight per rank (bench.py at N > 1: 3)")
     ap.add_argument("--world", type=int, default=8)
     a = ap.parse_args()
     import torch
@@ -62,17 +63,29 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps * 1e3
 
-    # N = 1 as bench.py runs it (4 in flight, auto priorities)
+    # N = 1 as bench.py runs it (4 in flight, auto priorities), after a second of frames (clock ramp)
     fr1 = FrameRenderer(scene, W, H, a.depth, precision="f32", inflight=4)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 1.0:
+        for _ in range(8):
+            fr1.launch()
+        torch.cuda.synchronize()
     res["n1_frame_ms"] = round(per_frame(fr1), 4)
     fr1.close()
+    # shard 0 of ns with k frames in flight (more frames hide more of a small shard's latency-bound tail)
+    sweep = {}
+    for k in (2, 3, 4, 6, 8):
+        fk = FrameRenderer(scene, W, H, a.depth, rank=0, world=ns, precision="f32", inflight=k)
+        sweep[k] = round(per_frame(fk), 4)
+        fk.close()
+    res["shard0_frame_ms_by_inflight"] = sweep
 
     codec = SlabCodec(W, H, 16, ns, "f32")
     rows = fr_rows = None
     shard_ms, shard_pack_ms, values_bytes = [], [], []
     headers, values = [], []
     for s in range(ns):
-        fr = FrameRenderer(scene, W, H, a.depth, rank=s, world=ns, precision="f32", inflight=3)
+        fr = FrameRenderer(scene, W, H, a.depth, rank=s, world=ns, precision="f32", inflight=a.inflight)
         fr_rows = fr.rows
         shard_ms.append(round(per_frame(fr), 4))
         # one header / values buffer per slot: packs of frames in flight must not share them (a
@@ -141,6 +154,7 @@ def main():
                        "a rank's render + pack" if floor == max(shard_pack_ms) else "rank 0's inbound links")
     res["projected_speedup_vs_n1"] = round(res["n1_frame_ms"] / floor, 2)
     res["north_star_speedup"] = 6.0
+    res["inflight"] = a.inflight
     print(json.dumps(res), flush=True)
 
 

@@ -411,7 +411,7 @@ def test_launch_writes_only_image_rows(name, spp):
 # ---- compact slab transfer (rt_slab_pack / rt_slab_unpack; dist.CompactGather) ----------
 @pytest.mark.parametrize("prec", ["f32", "f64"])
 @pytest.mark.parametrize("w,h,rb,ns", [(80, 70, 16, 3), (64, 64, 16, 1), (33, 17, 4, 2), (100, 9, 16, 8),
-                                       (257, 31, 5, 4)])
+                                       (257, 31, 5, 4), (2052, 40, 16, 8), (1024, 33, 7, 3)])
 def test_slab_codec_matches_reference_format(prec, w, h, rb, ns):
     """HIP pack gives the header and values of the test-side restatement byte for byte, on
     random sparse slabs (-0.0 and NaN payloads count as non-zero; padding rows hold garbage);
