@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-boundary", action="store_true")
     ap.add_argument("--inflight", type=int, default=None,
-                    help="frames in flight per rank (default 4 at N=1, 3 at N>1; 1 for --gather dense)")
+                    help="frames in flight per rank (default 4; 1 for --gather dense at N>1)")
     ap.add_argument("--priorities", default="auto",
                     help="comma-separated stream priority per in-flight slot (torch: lower = higher priority; "
                          "auto: FrameRenderer's default, half the slots high with >= 4 in flight and spp 1; none)")
@@ -257,7 +257,7 @@ def main():
     H = args.height or args.size
     scene = scenes.named(args.scene)
     counts = workload.scene_counts(scene)
-    inflight = args.inflight or (1 if args.gather == "dense" and world > 1 else 4 if world == 1 else 3)
+    inflight = args.inflight or (1 if args.gather == "dense" and world > 1 else 4)
     fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
                        precision=args.precision, order=args.order, spp=args.spp, seed=args.seed, inflight=inflight,
                        priorities=("auto" if args.priorities == "auto" else None if args.priorities == "none" else

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--inflight", type=int, default=3, help="frames in flight per rank (bench.py at N > 1: 3)")
+    ap.add_argument("--sweep", default="2,3,4,6,8", help="frames in flight tried for shard 0")
     ap.add_argument("--world", type=int, default=8)
     a = ap.parse_args()
     import torch
@@ -74,7 +75,7 @@ def main():
     fr1.close()
     # shard 0 of ns with k frames in flight (more frames hide more of a small shard's latency-bound tail)
     sweep = {}
-    for k in (2, 3, 4, 6, 8):
+    for k in [int(x) for x in a.sweep.split(",")]:
         fk = FrameRenderer(scene, W, H, a.depth, rank=0, world=ns, precision="f32", inflight=k)
         sweep[k] = round(per_frame(fk), 4)
         fk.close()
