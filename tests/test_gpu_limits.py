@@ -101,3 +101,59 @@ def test_thousands_of_spheres_rows_and_brute_force(oracle, name):
     fast = bench_frames(scene, w, h, d)
     assert nonbitwise(fast, img) == 0
     assert nonbitwise(fast, bench_frames(scene, w, h, d, cull=False)) == 0
+
+
+def test_update_scene_equals_fresh_context_and_times_pmask():
+    """rt_update_scene (an animated scene: one sphere moved per frame, as bench.py's setup leg does)
+    renders bit for bit what a fresh context renders for the same scene — the per-origin tables,
+    occluder masks and the primary rays' candidate masks (k_pmask, rebuilt after the update, timed
+    through RT_KT_PMASK) all follow the new scene; and a scene of another size in place of S64."""
+    import ctypes
+
+    import torch
+    L = N.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    w, h, d = 320, 240, 5
+
+    def frame(p):
+        out = torch.full((h, w, 3), float("nan"), dtype=torch.float64, device="cuda")
+        N.check(L.rt_launch(p, w, h, d, 16, 0, 1, N.RT_OUT_F64, N.RT_ORDER_EXACT, out.data_ptr(), None, st))
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+
+    el = N.marshal(scenes.s64())
+    p = ctypes.c_void_p()
+    N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(p)), "rt_prepare")
+    try:
+        N.check(L.rt_configure(p, N.RT_CFG_SIDE_STREAMS, 0), "rt_configure")
+        N.check(L.rt_configure(p, N.RT_CFG_KERNEL_TIMING, N.RT_KT_PMASK), "rt_configure")
+        first = frame(p)
+        k = [i for i in range(len(el)) if el[i].kind == N.RT_SPHERE][0]
+        scenes_ = []
+        for s in range(3):
+            el[k].u.sphere.center.x += 0.75  # moves across other spheres' cones: different masks
+            el[k].canon = -1
+            N.check(L.rt_update_scene(p, el, len(el)), "rt_update_scene")
+            got = frame(p)
+            q = ctypes.c_void_p()
+            N.check(L.rt_prepare(el, len(el), 0, ctypes.byref(q)), "rt_prepare")
+            try:
+                ref = frame(q)
+            finally:
+                L.rt_release(q)
+            assert nonbitwise(got, ref) == 0, f"step {s}"
+            scenes_.append(got)
+        assert nonbitwise(scenes_[0], first) > 0  # the sphere really moved
+        ms, n = ctypes.c_double(0), ctypes.c_uint64(0)
+        N.check(L.rt_kernel_time(p, N.RT_KT_PMASK, ctypes.byref(ms), ctypes.byref(n), 1), "rt_kernel_time")
+        assert n.value == 4 and ms.value > 0  # one k_pmask per scene (the first and three updates)
+        other = N.marshal(scenes.named("s300"))
+        N.check(L.rt_update_scene(p, other, len(other)), "rt_update_scene")
+        q = ctypes.c_void_p()
+        N.check(L.rt_prepare(other, len(other), 0, ctypes.byref(q)), "rt_prepare")
+        try:
+            assert nonbitwise(frame(p), frame(q)) == 0
+        finally:
+            L.rt_release(q)
+    finally:
+        L.rt_release(p)
