@@ -83,6 +83,9 @@ def parse():
                          "default: 0 at --gpus 1, 8 with more)")
     ap.add_argument("--no-setup", action="store_true",
                     help="skip the setup-cost leg (scene compile, primary masks, new-scene and cold frames)")
+    ap.add_argument("--rank0", default="auto", choices=["auto", "render", "assemble"],
+                    help="N > 1: rank 0 renders its share of rows (render) or only reassembles the frame while ranks "
+                         "1..N-1 render (assemble); auto: assemble from 4 ranks on (compact gather only)")
     ap.add_argument("--gather", default="compact", choices=["compact", "dense"],
                     help="N > 1: compact = background pixels not sent (rt_slab_pack, default); dense = whole slabs")
     return ap.parse_args()
@@ -258,19 +261,27 @@ def main():
     scene = scenes.named(args.scene)
     counts = workload.scene_counts(scene)
     inflight = args.inflight or (1 if args.gather == "dense" and world > 1 else 4)
+    # Rank 0 as assembler (N >= 4 by default): at N = 8 a rank renders its shard in ~0.1 ms, and rank 0
+    # rendering one too while it decodes the whole frame was the slowest stage
+    assemble = world > 1 and args.gather == "compact" and (args.rank0 == "assemble" or
+                                                          (args.rank0 == "auto" and world >= 4))
     fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
                        precision=args.precision, order=args.order, spp=args.spp, seed=args.seed, inflight=inflight,
                        priorities=("auto" if args.priorities == "auto" else None if args.priorities == "none" else
-                                   parse_priorities(args.priorities)))
+                                   parse_priorities(args.priorities)), assemble=assemble)
 
     # untimed: work count of this rank's rows (levels of every pixel's reflection chain)
     lv_fr = FrameRenderer(scene, W, H, args.depth, rank=rank, world=world, device=local, row_block=args.row_block,
-                          precision=args.precision, order=args.order, levels=True)
-    lv_fr.launch()
-    torch.cuda.synchronize()
+                          precision=args.precision, order=args.order, levels=True, assemble=assemble)
     from eraytracer_amd.dist import shard_global_rows
-    valid = torch.from_numpy(shard_global_rows(H, args.row_block, world, rank) >= 0).to(lv_fr.levels.device)
-    hist = torch.bincount(lv_fr.levels[valid].flatten().to(torch.int64), minlength=args.depth + 1).cpu().numpy()
+    if lv_fr.renders:
+        lv_fr.launch()
+        torch.cuda.synchronize()
+        valid = torch.from_numpy(shard_global_rows(H, args.row_block, lv_fr.nshards, lv_fr.shard) >= 0)
+        valid = valid.to(lv_fr.levels.device)
+        hist = torch.bincount(lv_fr.levels[valid].flatten().to(torch.int64), minlength=args.depth + 1).cpu().numpy()
+    else:  # an assembling rank 0 renders no pixels
+        hist = np.zeros(args.depth + 1, dtype=np.int64)
     lv_fr.close()
     del lv_fr
     # with spp > 1 the work is estimated as spp times that of the unjittered frame
@@ -297,7 +308,7 @@ def main():
             fr.gather()
         elif args.gather == "compact":
             with torch.cuda.stream(fr.stream):
-                pipe.submit(fr.slab, rank)
+                pipe.submit(fr.slab if fr.renders else None, fr.shard)
         else:
             pipe.submit()
 
@@ -456,7 +467,8 @@ def main():
                        "framebuffer": args.precision, "row_block": args.row_block, "inflight": inflight,
                        "engine": engine,
                        "stream_priorities": [st.priority for st in fr.streams] if fr.streams else None,
-                       "parallelism": f"rows{world}" + (f"+rccl_{args.gather}_gather" if world > 1 else ""),
+                       "parallelism": f"rows{world - 1 if assemble else world}" + (f"+rccl_{args.gather}_gather" if world > 1 else "")
+                       + ("+rank0_assembles" if assemble else ""),
                        "world_size": world, "rccl_ranks": dist.get_world_size() if world > 1 else 1,
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4),
                        "spheres": counts["spheres"], "triangles": counts["triangles"], "planes": counts["planes"],
@@ -517,9 +529,11 @@ def self_check(fr, pipe, scene, args, rank, world, local):
     depths = [1, 2]
 
     def make_slab(i):
+        if not fr.renders:  # an assembling rank 0
+            return None
         slab = fr.slabs[0]
-        N.check(L.rt_launch_spp(fr._ps[0], fr.w, fr.h, depths[i], fr.rb, rank, world, fr.prec, fr.order, fr.spp,
-                                fr.seed, slab.data_ptr(), None, torch.cuda.current_stream().cuda_stream))
+        N.check(L.rt_launch_spp(fr._ps[0], fr.w, fr.h, depths[i], fr.rb, fr.shard, fr.nshards, fr.prec, fr.order,
+                                fr.spp, fr.seed, slab.data_ptr(), None, torch.cuda.current_stream().cuda_stream))
         return slab
 
     def reference(i):
@@ -535,7 +549,7 @@ def self_check(fr, pipe, scene, args, rank, world, local):
         finally:
             L.rt_release(p)
 
-    n = verify_compact_gather(pipe, make_slab, reference, rank, nframes=len(depths))
+    n = verify_compact_gather(pipe, make_slab, reference, rank, nframes=len(depths), shard=fr.shard)
     torch.cuda.synchronize()
     return {"frames": n, "equal_bitwise": True, "what": "compact-gathered frames == one-shard rt_launch frames"} \
         if rank == 0 else None

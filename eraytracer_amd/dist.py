@@ -165,20 +165,26 @@ class CompactGather:
     i-4's send (rank 0: its decode), so the caller may render consecutive frames on different
     streams; every collective is issued on the side stream behind an event of the pack it
     reads, so it never waits for a later render.
+
+    ``first`` = 1: rank 0 renders no rows and only assembles (the codec's shards are ranks 1 ..
+    world-1, shard = rank - 1); it submits None and its header in the gather is ignored.
     """
 
     RING = 4
     LAG = 2  # frames between a frame's header gather and its value transfer
 
-    def __init__(self, codec, world, rank, slab_elems, dtype, device, frame, group=None):
+    def __init__(self, codec, world, rank, slab_elems, dtype, device, frame, group=None, first=0):
         import torch
         self.torch = torch
         self.codec, self.world, self.rank, self.group = codec, world, rank, group
+        if first not in (0, 1) or (first == 1 and world < 2):
+            raise ValueError("first: 0 (every rank renders) or 1 (rank 0 assembles; world >= 2)")
+        self.first = first
         self.frame = frame
         self.cuda = torch.device(device).type == "cuda"
         hb = codec.header_bytes
         mk = lambda *shape, dt: torch.empty(shape, dtype=dt, device=device)  # noqa: E731
-        self.hdr = [mk(hb, dt=torch.uint8) for _ in range(self.RING)]
+        self.hdr = [torch.zeros(hb, dtype=torch.uint8, device=device) for _ in range(self.RING)]
         self.vals = [mk(slab_elems, dt=dtype) for _ in range(self.RING)]
         self.ghdr = self.gvals = None
         if rank == 0:
@@ -197,13 +203,18 @@ class CompactGather:
         return self.torch.cuda.stream(self.xs) if self.cuda else contextlib.nullcontext()
 
     def submit(self, slab, shard):
+        """Hand over the slab of this rank's shard `shard` just rendered (None on an assembling
+        rank 0, which renders nothing)."""
         torch = self.torch
         b = self.i % self.RING
         self.i += 1
         if self.free[b] is not None:  # slot b's last send / decode has read its buffers
             torch.cuda.current_stream().wait_event(self.free[b])
             self.free[b] = None
-        self.codec.pack(slab, shard, self.hdr[b], self.vals[b])
+        if slab is not None:
+            self.codec.pack(slab, shard, self.hdr[b], self.vals[b])
+        elif not (self.first == 1 and self.rank == 0):
+            raise ValueError("only an assembling rank 0 submits no slab")
         ev = None
         if self.cuda:
             ev = torch.cuda.Event()
@@ -277,9 +288,9 @@ class CompactGather:
         with self._side():
             for w in works:
                 w.wait()
-            if self.rank == 0:
-                vals = [self.vals[b]] + [self.gvals[b][s] for s in range(1, self.world)]
-                self.codec.unpack(list(self.ghdr[b].unbind(0)), vals, self.frame)
+            if self.rank == 0:  # the rendering ranks' shards: ranks first .. world-1
+                vals = ([self.vals[b]] if self.first == 0 else []) + [self.gvals[b][s] for s in range(1, self.world)]
+                self.codec.unpack(list(self.ghdr[b].unbind(0))[self.first:], vals, self.frame)
             if self.cuda:
                 ev = self.torch.cuda.Event()
                 ev.record()
@@ -289,12 +300,14 @@ class CompactGather:
         return self.frame if self.rank == 0 else None
 
 
-def verify_compact_gather(cg, make_slab, reference, rank, nframes=2):
+def verify_compact_gather(cg, make_slab, reference, rank, nframes=2, shard=None):
     """The multi-rank bench's self-check before timing: every rank renders its slab of a check
-    frame (``make_slab(i)``, frame i), the slabs go through the compact gather ``cg`` exactly as
-    in the timed loop (frames in flight), and rank 0 compares every reassembled frame bit for
-    bit with ``reference(i)`` (a one-shard render of the same frame).  Raises on a mismatch;
-    returns the number of frames checked on rank 0 (0 elsewhere)."""
+    frame (``make_slab(i)``, frame i; None on an assembling rank 0), the slabs go through the
+    compact gather ``cg`` exactly as in the timed loop (frames in flight), and rank 0 compares
+    every reassembled frame bit for bit with ``reference(i)`` (a one-shard render of the same
+    frame).  ``shard``: this rank's shard (default: its rank).  Raises on a mismatch; returns the
+    number of frames checked on rank 0 (0 elsewhere)."""
+    shard = rank if shard is None else shard
     import torch
     got = []
 
@@ -306,7 +319,7 @@ def verify_compact_gather(cg, make_slab, reference, rank, nframes=2):
             torch.cuda.synchronize()
 
     for i in range(nframes):
-        out = cg.submit(make_slab(i), rank)
+        out = cg.submit(make_slab(i), shard)
         if out is not None:
             keep(out)
     cg.drain(on_frame=keep)
@@ -343,18 +356,25 @@ class FrameRenderer:
     def __init__(self, scene, width: int, height: int, depth: int, *, rank: int = 0, world: int = 1,
                  device: int = 0, row_block: int = 16, precision: str = "f32", order: str = "exact", group=None,
                  levels: bool = False, spp: int = 1, seed: int = 0, inflight: int = 1, cull: bool = True,
-                 priorities="auto"):
+                 priorities="auto", assemble: bool = False):
         import torch
         self.torch = torch
         self.L = N.lib()
         self.w, self.h, self.depth = width, height, depth
         self.rank, self.world, self.rb, self.group = rank, world, row_block, group
+        # assemble (world > 1): rank 0 renders no rows and only reassembles the frame; ranks 1 ..
+        # world-1 render shards 0 .. world-2.  Rank 0 keeps contexts of shard 0's geometry for
+        # launch_on (timing) only: launch() renders nothing there.
+        self.assemble = bool(assemble) and world > 1
+        self.nshards = world - 1 if self.assemble else world
+        self.shard = max(rank - 1, 0) if self.assemble else rank
+        self.renders = not (self.assemble and rank == 0)
         self.spp, self.seed = spp, seed
         self.prec, self.order = PRECISIONS[precision], ORDERS[order]
         self.precision = precision
         self.dtype = torch.float64 if precision == "f64" else torch.float32
         self.device = torch.device("cuda", device)
-        self.rows = shard_rows(height, row_block, world)
+        self.rows = shard_rows(height, row_block, self.nshards)
         if inflight < 1 or (inflight > 1 and levels):
             raise ValueError("inflight must be >= 1 (and 1 with levels)")
         el = N.marshal(scene)
@@ -394,7 +414,8 @@ class FrameRenderer:
         self.gather_buf = None
         self.frame = None
         if world > 1 and rank == 0:
-            self.gather_buf = torch.empty((world, self.rows, width, 3), dtype=self.dtype, device=self.device)
+            if not self.assemble:  # (the dense gather's buffer; the compact gather has its own)
+                self.gather_buf = torch.empty((world, self.rows, width, 3), dtype=self.dtype, device=self.device)
             self.frame = torch.empty((height, width, 3), dtype=self.dtype, device=self.device)
         self._pipe = None
         self._cg = None
@@ -408,16 +429,18 @@ class FrameRenderer:
             self.slab, self.stream = self.slabs[j], self.streams[j]
         else:
             self.stream = self.torch.cuda.current_stream(self.device)
+        if not self.renders:  # an assembling rank 0
+            return
         lv = self.levels.data_ptr() if self.levels is not None else None
-        N.check(self.L.rt_launch_spp(self._ps[j], self.w, self.h, self.depth, self.rb, self.rank, self.world, self.prec,
-                                     self.order, self.spp, self.seed, self.slab.data_ptr(), lv,
+        N.check(self.L.rt_launch_spp(self._ps[j], self.w, self.h, self.depth, self.rb, self.shard, self.nshards,
+                                     self.prec, self.order, self.spp, self.seed, self.slab.data_ptr(), lv,
                                      self.stream.cuda_stream), "rt_launch")
 
     def launch_on(self, j: int):
         """Render a frame on slot j's context, slab and stream (no gather)."""
         stream = self.streams[j] if self.streams is not None else self.torch.cuda.current_stream(self.device)
-        N.check(self.L.rt_launch_spp(self._ps[j], self.w, self.h, self.depth, self.rb, self.rank, self.world, self.prec,
-                                     self.order, self.spp, self.seed, self.slabs[j].data_ptr(), None,
+        N.check(self.L.rt_launch_spp(self._ps[j], self.w, self.h, self.depth, self.rb, self.shard, self.nshards,
+                                     self.prec, self.order, self.spp, self.seed, self.slabs[j].data_ptr(), None,
                                      stream.cuda_stream), "rt_launch")
 
     def time_kernels(self, mask: int):
@@ -456,6 +479,8 @@ class FrameRenderer:
     def gather(self):
         if self.world == 1:
             return self.slab
+        if self.assemble:
+            raise ValueError("an assembling rank 0 takes the compact gather (compact_gather)")
         import torch.distributed as dist
         if self.rank == 0:
             dist.gather(self.slab, gather_list=list(self.gather_buf.unbind(0)), dst=0, group=self.group)
@@ -472,6 +497,8 @@ class FrameRenderer:
 
     # ---- pipelined frames (world > 1): render frame i+1 while frame i is gathered ----------
     def pipeline(self):
+        if self.assemble:
+            raise ValueError("an assembling rank 0 takes the compact gather (compact_gather)")
         if self.streams is not None:
             raise ValueError("the dense slab pipeline takes one frame in flight (inflight=1)")
         if self._pipe is None:
@@ -501,9 +528,9 @@ class FrameRenderer:
     # ---- compact gather (world > 1, the default in bench.py): background pixels not sent ----
     def compact_gather(self):
         if self._cg is None:
-            codec = SlabCodec(self.w, self.h, self.rb, self.world, self.precision)
+            codec = SlabCodec(self.w, self.h, self.rb, self.nshards, self.precision)
             self._cg = CompactGather(codec, self.world, self.rank, self.slab.numel(), self.dtype, self.device,
-                                     self.frame, self.group)
+                                     self.frame, self.group, first=1 if self.assemble else 0)
         return self._cg
 
     def step_compact(self):
@@ -512,7 +539,7 @@ class FrameRenderer:
         cg = self.compact_gather()
         self.launch()
         with self.torch.cuda.stream(self.stream):
-            return cg.submit(self.slab, self.rank)
+            return cg.submit(self.slab if self.renders else None, self.shard)
 
     def drain_compact(self):
         return self._cg.drain() if self._cg is not None else None

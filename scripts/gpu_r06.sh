@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-6 GPU steps (each under its own time limit; the first failure ends the call).
 #   bash scripts/gpu_r06.sh TAG lim       the input-size tests (depth, lights, objects) alone
+#   VARIANTS="- a b" CFGS="c3dq c5q" REPS=2 bash scripts/gpu_r06.sh TAG ab   A/B of library variants
 #   bash scripts/gpu_r06.sh TAG test      GPU parity suite, then the RT_DEBUG_LISTS build's wavefront tests
 #   bash scripts/gpu_r06.sh TAG bench     bench lines: config 3 (driver-style 20/5 and default), configs 2, 5
 #   bash scripts/gpu_r06.sh TAG c3        config 3 driver-style bench line only
@@ -15,7 +16,28 @@ export PYTHONUNBUFFERED=1
 C2="--scene default --width 1920 --height 1080 --depth 5"
 C5="--scene s256 --depth 8 --spp 16"
 b() { name=$1; shift; timeout -k 10 300 python bench.py "$@" > gpurun_out/${TAG}_bench_$name.json 2> gpurun_out/${TAG}_bench_$name.err || { tail -5 gpurun_out/${TAG}_bench_$name.err; exit 1; }; python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], d['value'], 'Mpx/s', d['ms_per_step'], 'ms/frame', 'dom', r.get('launch_ms_live'), 'frac', r.get('frac'), 'cpu', d.get('cpu_baseline', {}).get('value'), d.get('cpu_baseline', {}).get('cores'))" gpurun_out/${TAG}_bench_$name.json $name; }
+cfg_args() {
+  case $1 in
+    c2q) echo "$C2 --no-cpu-baseline --no-boundary --no-setup" ;;
+    c3q) echo "--no-cpu-baseline --no-boundary --no-setup" ;;
+    c3dq) echo "--steps 20 --warmup 5 --no-cpu-baseline --no-boundary --no-setup" ;;
+    c5q) echo "$C5 --steps 8 --warmup 3 --no-boundary --no-cpu-baseline --no-setup" ;;
+  esac
+}
 case $PART in
+ab)
+  # A/B of library variants: VARIANTS="- name ..." (eraytracer_amd/variants/librtmi355x_NAME.so; - = default)
+  : > gpurun_out/${TAG}_ab.txt
+  for rep in $(seq 1 ${REPS:-2}); do
+    for c in ${CFGS:-c3dq c5q}; do
+      for v in ${VARIANTS:--}; do
+        lib=""; [ "$v" = "-" ] || lib="eraytracer_amd/variants/librtmi355x_$v.so"
+        RT_LIB_PATH=$lib timeout -k 10 300 python bench.py $(cfg_args $c) > gpurun_out/${TAG}_ab_one.json 2> gpurun_out/${TAG}_ab_one.err \
+          || { tail -5 gpurun_out/${TAG}_ab_one.err; exit 1; }
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d.get('roofline',{}); print(sys.argv[2], d['value'], 'Mpx/s', d['ms_per_step'], 'ms/frame', 'dom', r.get('launch_ms_live'))" gpurun_out/${TAG}_ab_one.json "$c $v rep$rep" | tee -a gpurun_out/${TAG}_ab.txt || exit 1
+      done
+    done
+  done ;;
 lim)
   make -C oracle > /dev/null || exit 1
   timeout -k 10 900 python -u -m pytest tests/test_gpu_limits.py -x -v -m gpu --timeout 400 --timeout-method thread > gpurun_out/pytest_lim_$TAG.log 2>&1 || { tail -40 gpurun_out/pytest_lim_$TAG.log; exit 1; }

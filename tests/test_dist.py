@@ -233,3 +233,50 @@ def test_gloo_bench_self_check(tmp_path, world, corrupt):
         assert res.startswith("error") and "frame 1" in res and "1 pixels" in res, res
     else:
         assert res == "ok 3", res
+
+
+def _assemble_worker(rank, world, port, out_path, nframes):
+    """CompactGather with an assembling rank 0: ranks 1 .. world-1 render shards 0 .. world-2 of
+    world-1; rank 0 submits nothing and decodes."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eraytracer_amd.dist import CompactGather
+    from tests.slab_ref import RefCodec
+    ns = world - 1
+    rows = shard_rows(H, RB, ns)
+    codec = RefCodec(W, H, RB, ns)
+    frame = torch.empty((H, W, 3), dtype=torch.float32) if rank == 0 else None
+    cg = CompactGather(codec, world, rank, rows * W * 3, torch.float32, "cpu", frame, first=1)
+    frames = []
+    for f in range(nframes):
+        slab = None if rank == 0 else _sparse_slab(f, rank - 1, ns, rows)
+        out = cg.submit(slab, max(rank - 1, 0))
+        if out is not None:
+            frames.append(out.clone())
+    cg.drain(on_frame=lambda fr: frames.append(fr.clone()))
+    if rank == 0:
+        np.save(out_path, torch.stack(frames).numpy())
+    else:
+        assert not frames
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_gloo_compact_gather_with_assembling_rank0(tmp_path, world):
+    """bench.py --rank0 assemble (the default from 4 ranks): rank 0 renders no rows, the other ranks'
+    shards arrive complete, exact and in order."""
+    out = str(tmp_path / "frames.npy")
+    nframes = 6
+    mp.spawn(_assemble_worker, args=(world, _free_port(), out, nframes), nprocs=world, join=True)
+    frames = np.load(out)
+    assert frames.shape == (nframes, H, W, 3)
+    for f in range(nframes):
+        assert np.array_equal(frames[f].view(np.int32), _expected_frame(f).numpy().view(np.int32)), f"frame {f}"
+
+
+def test_assembling_rank0_must_submit_nothing():
+    from eraytracer_amd.dist import CompactGather
+    from tests.slab_ref import RefCodec
+    with pytest.raises(ValueError):
+        CompactGather(RefCodec(W, H, RB, 1), 1, 0, 10, torch.float32, "cpu", None, first=1)

@@ -610,3 +610,43 @@ def test_fused_reflect_shade_matches_oracle(oracle, name, w, h, d):
     assert np.array_equal(outs[0].view(np.int64), outs[1].view(np.int64))
     ref, _ = _oracle(oracle, scene, w, h, d)
     _check(outs[1], ref)
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_assembling_rank0_shards_reassemble(world):
+    """bench.py --rank0 assemble on one device: FrameRenderer(assemble=True) ranks 1 .. world-1
+    render shards 0 .. world-2 of world-1 (packed and decoded as rank 0 would), equal to the
+    one-shard frame bit for bit; rank 0's launch() renders nothing."""
+    import torch
+
+    from eraytracer_amd.dist import FrameRenderer, SlabCodec
+    w, h, d = 160, 100, 5
+    one = FrameRenderer(scenes.s64(), w, h, d, precision="f32")
+    one.launch()
+    torch.cuda.synchronize()
+    ref = one.slab[:h].clone()
+    one.close()
+    codec = SlabCodec(w, h, 16, world - 1, "f32")
+    hdrs, vals = [], []
+    for r in range(world):
+        fr = FrameRenderer(scenes.s64(), w, h, d, rank=r, world=world, precision="f32", inflight=2, assemble=True)
+        try:
+            assert fr.nshards == world - 1 and fr.shard == max(r - 1, 0) and fr.renders == (r > 0)
+            for s in fr.slabs:
+                s.fill_(float("nan"))
+            fr.fork()
+            fr.launch()
+            fr.join()
+            torch.cuda.synchronize()
+            if r == 0:
+                assert bool(torch.isnan(fr.slabs[0]).all()), "rank 0 rendered rows"
+                continue
+            hdrs.append(torch.empty(codec.header_bytes, dtype=torch.uint8, device="cuda"))
+            vals.append(torch.empty(fr.rows * w * 3, dtype=torch.float32, device="cuda"))
+            codec.pack(fr.slabs[0], fr.shard, hdrs[-1], vals[-1])
+        finally:
+            fr.close()
+    img = torch.full((h, w, 3), -1.0, dtype=torch.float32, device="cuda")
+    codec.unpack(hdrs, vals, img)
+    torch.cuda.synchronize()
+    assert torch.equal(img.view(torch.int32), ref.view(torch.int32))
