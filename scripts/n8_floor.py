@@ -156,6 +156,12 @@ def main():
     res["projected_speedup_vs_n1"] = round(res["n1_frame_ms"] / floor, 2)
     res["north_star_speedup"] = 6.0
     res["inflight"] = a.inflight
+    # the same shards with an assembling rank 0 (bench.py --rank0 assemble: world + 1 GPUs, rank 0
+    # renders nothing and only decodes): the slowest rendering rank, or rank 0's decode
+    asm = max(max(shard_pack_ms), res["unpack8_ms"], res["transfer_ms_at_link_peak"])
+    res["assembler_gpus"] = ns + 1
+    res["assembler_projected_step_ms"] = round(asm, 4)
+    res["assembler_projected_speedup_vs_n1"] = round(res["n1_frame_ms"] / asm, 2)
     print(json.dumps(res), flush=True)
 
 
