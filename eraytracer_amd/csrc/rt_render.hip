@@ -400,13 +400,34 @@ __device__ __forceinline__ double lane_f64(double v, int lane) { // v of `lane`,
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+// Across the four rows (RT_DPP_BCAST, A/B builds): row_bcast:15 (row_mask 0xA: rows 1 and 3 take lane 15 of
+// rows 0 and 2) then row_bcast:31 (row_mask 0xC: rows 2 and 3 take lane 31), so lane 63 holds the wave's
+// result and one readlane (two for binary64) reads it, instead of four (eight) and three more operations.
+// Rows the mask leaves out keep their own value (`old`); only lane 63's chain matters.
+#ifndef RT_DPP_BCAST
+#define RT_DPP_BCAST 0 // 1: measured within noise on configs 3 and 5 (profiles/r06m_ab_dpp_row_bcast.txt)
+#endif
+constexpr int DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143;
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64_rows(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp((int)b, (int)b, CTRL, ROWS, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), CTRL, ROWS, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
 template <typename Op>
 __device__ __forceinline__ double wave_reduce(double v, Op op) {
     v = op(v, dpp_f64<DPP_XOR1>(v));
     v = op(v, dpp_f64<DPP_XOR2>(v));
     v = op(v, dpp_f64<DPP_HALF_MIRROR>(v));
     v = op(v, dpp_f64<DPP_MIRROR>(v));
+#if RT_DPP_BCAST
+    v = op(v, dpp_f64_rows<DPP_ROW_BCAST15, 0xA>(v));
+    v = op(v, dpp_f64_rows<DPP_ROW_BCAST31, 0xC>(v));
+    return lane_f64(v, 63);
+#else
     return op(op(lane_f64(v, 0), lane_f64(v, 16)), op(lane_f64(v, 32), lane_f64(v, 48)));
+#endif
 }
 __device__ __forceinline__ double wave_sum(double v) {
     return wave_reduce(v, [](double a, double b) { return a + b; });
@@ -545,7 +566,13 @@ __device__ __forceinline__ float wave_reduce32(float v, Op op) {
     v = op(v, dpp_f32<DPP_XOR2>(v));
     v = op(v, dpp_f32<DPP_HALF_MIRROR>(v));
     v = op(v, dpp_f32<DPP_MIRROR>(v));
+#if RT_DPP_BCAST // (see wave_reduce)
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), DPP_ROW_BCAST15, 0xA, 0xF, false)));
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), DPP_ROW_BCAST31, 0xC, 0xF, false)));
+    return lane_f32(v, 63);
+#else
     return op(op(lane_f32(v, 0), lane_f32(v, 16)), op(lane_f32(v, 32), lane_f32(v, 48)));
+#endif
 }
 // Must be called with the whole wave converged.  o, d: the lanes' ray origins and directions.
 __device__ __forceinline__ Beam32 make_beam32(const SceneHdr &h, bool act, const D3 &o, const D3 &d) {
