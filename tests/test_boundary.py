@@ -110,6 +110,23 @@ def test_no_count_limits(native):
         assert L.rt_scene_check(el, len(el)) == N.RT_OK
 
 
+def test_tables_past_32_bit_offsets_are_enomem(native):
+    """The only size limit left (include/rt_mi355x.h): a scene whose per-origin tables (about 16
+    doubles per origin and object; the origins are the camera and every light) would not fit the
+    kernels' 32-bit offsets fails with RT_ENOMEM — from the host compiler, before any device call,
+    so this runs on the CPU."""
+    import ctypes
+    L = native.lib()
+    base = scenes.s64()
+    light = [t for t in base if t[0] == "point_light"][0]
+    spheres = [t for t in base if t[0] == "sphere"]
+    scene = base[:1] + [light] * 70000 + spheres * 16  # 70,001 origins x 1,024 spheres (copies: canon)
+    el = N.marshal(scene)
+    assert L.rt_scene_check(el, len(el)) == N.RT_OK
+    p = ctypes.c_void_p()
+    assert L.rt_prepare(el, len(el), 0, ctypes.byref(p)) == N.RT_ENOMEM
+
+
 def test_scene_canon_large_matches_prefix_rule(native):
     """rt_scene_canon (hashed) against the definition — the first earlier self-canonical element of
     the same kind with the same payload bytes — on a 3,000-element list with planted duplicates

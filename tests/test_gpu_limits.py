@@ -157,3 +157,40 @@ def test_update_scene_equals_fresh_context_and_times_pmask():
             L.rt_release(q)
     finally:
         L.rt_release(p)
+
+
+def test_more_spheres_than_the_bvh_holds(oracle):
+    """S70000: more spheres than the BVH's 16-bit links hold (BVH_MAX_SPHERES) and far more occluder
+    tests than the budget — no BVH, no occluder masks: the reflection scans walk 1,094 beam-culled
+    chunks, the shadow rays the shadow cones.  48x32 depth 3, every pixel against the oracle and
+    bit for bit against brute force."""
+    scene = scenes.named("s70000")
+    w, h, d = 48, 32, 3
+    img, lv = render(w, h, scene, d, levels=True)
+    ref, rlv = oracle.render(N.marshal(scene), w, h, d, mode=oracle.MEMO, levels=True)
+    np.testing.assert_array_equal(lv, rlv)
+    assert float(np.abs(img - ref).max()) <= TOL
+    fast = bench_frames(scene, w, h, d)
+    assert nonbitwise(fast, img) == 0
+    assert nonbitwise(fast, bench_frames(scene, w, h, d, cull=False)) == 0
+
+
+def test_thousand_lights(oracle):
+    """1,000 point lights over 16 spheres (the fused engine folding every light, shadow words far
+    past 32 bits), 48x36 depth 3, against the oracle."""
+    scene = scenes.synthetic_scene(16, 0x5EED1000, n_lights=1000)
+    img, lv = render(48, 36, scene, 3, levels=True)
+    ref, rlv = oracle.render(N.marshal(scene), 48, 36, 3, mode=oracle.MEMO, levels=True)
+    np.testing.assert_array_equal(lv, rlv)
+    assert float(np.abs(img - ref).max()) <= TOL
+
+
+def test_depth_one_thousand(oracle):
+    """Depth 1,000 on the one-light default scene (its endless chains reflect a thousand times:
+    a thousand levels of queues and launches), 32x24, against the oracle; levels saturate at 255."""
+    scene = _one_light_default()
+    img, lv = render(32, 24, scene, 1000, levels=True)
+    ref, rlv = oracle.render(N.marshal(scene), 32, 24, 1000, mode=oracle.MEMO, levels=True)
+    np.testing.assert_array_equal(lv, rlv)
+    assert float(np.abs(img - ref).max()) <= TOL
+    assert int(lv.max()) == 255
