@@ -44,8 +44,10 @@ lim)
   grep -E "PASS|FAIL|depth|passed|failed" gpurun_out/pytest_lim_$TAG.log | tail -20 ;;
 test)
   make -C oracle > /dev/null || exit 1
-  timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_$TAG.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_$TAG.log; exit 1; }
   tail -1 gpurun_out/pytest_$TAG.log
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -5 gpurun_out/smoke_$TAG.log; exit 1; }
+  tail -1 gpurun_out/smoke_$TAG.log
   bash scripts/debug_lists.sh run > gpurun_out/debug_lists_$TAG.log 2>&1 || { tail -30 gpurun_out/debug_lists_$TAG.log; exit 1; }
   tail -1 gpurun_out/debug_lists_$TAG.log ;;
 c3)
