@@ -194,24 +194,27 @@ def test_ref_codec_round_trip_and_layout():
         assert torch.equal(frame.view(torch.int32), _expected_frame(2).view(torch.int32))
 
 
-def _verify_worker(rank, world, port, out_path, corrupt):
+def _verify_worker(rank, world, port, out_path, corrupt, first=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from eraytracer_amd.dist import CompactGather, verify_compact_gather
     from tests.slab_ref import RefCodec
-    rows = shard_rows(H, RB, world)
-    codec = RefCodec(W, H, RB, world)
+    ns, shard = world - first, max(rank - first, 0)  # first = 1: rank 0 assembles
+    rows = shard_rows(H, RB, ns)
+    codec = RefCodec(W, H, RB, ns)
     frame = torch.empty((H, W, 3), dtype=torch.float32) if rank == 0 else None
-    cg = CompactGather(codec, world, rank, rows * W * 3, torch.float32, "cpu", frame)
+    cg = CompactGather(codec, world, rank, rows * W * 3, torch.float32, "cpu", frame, first=first)
 
     def make_slab(i):
-        s = _sparse_slab(i, rank, world, rows)
+        if first and rank == 0:
+            return None
+        s = _sparse_slab(i, shard, ns, rows)
         if corrupt and rank == world - 1 and i == 1:
             s[0, 3] = 42.0  # one wrong pixel on the last rank
         return s
 
     try:
-        n = verify_compact_gather(cg, make_slab, _expected_frame, rank, nframes=3)
+        n = verify_compact_gather(cg, make_slab, _expected_frame, rank, nframes=3, shard=shard)
         res = f"ok {n}"
     except RuntimeError as e:
         res = f"error {e}"
@@ -222,12 +225,14 @@ def _verify_worker(rank, world, port, out_path, corrupt):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,corrupt", [(2, False), (3, False), (3, True)])
-def test_gloo_bench_self_check(tmp_path, world, corrupt):
+@pytest.mark.parametrize("world,corrupt,first", [(2, False, 0), (3, False, 0), (3, True, 0), (3, False, 1),
+                                                (4, True, 1)])
+def test_gloo_bench_self_check(tmp_path, world, corrupt, first):
     """bench.py --gpus N's check before timing (dist.verify_compact_gather): the compact gather's
-    frames equal the one-shard frames, and a single wrong pixel on any rank is caught."""
+    frames equal the one-shard frames, and a single wrong pixel on any rank is caught — also with
+    an assembling rank 0 (first = 1)."""
     out = str(tmp_path / "res.txt")
-    mp.spawn(_verify_worker, args=(world, _free_port(), out, corrupt), nprocs=world, join=True)
+    mp.spawn(_verify_worker, args=(world, _free_port(), out, corrupt, first), nprocs=world, join=True)
     res = open(out).read()
     if corrupt:
         assert res.startswith("error") and "frame 1" in res and "1 pixels" in res, res
