@@ -195,11 +195,12 @@ __device__ __forceinline__ void dd_mul(double &ah, double &al, double bh, double
 // GENPOW: the scene has a specular power outside {0, 1, ..., 1024} (decided on the host, see
 // pow_int_ok in rt_scene.cpp), so the general device pow is compiled in; otherwise its large
 // register footprint is kept out of the kernel.
-template <bool GENPOW>
-__device__ __forceinline__ double pow_libm(double x, double y) {
-    if (GENPOW && !(y >= 0.0 && y <= 1024.0 && y == __builtin_floor(y))) return pow(x, y);
-    unsigned n = (unsigned)y;
-    if (n == 0) return 1.0;
+// x^n, n >= 1, by binary powering (the operations depend on n alone).  BR (n wave-uniform): the
+// multiplications sit under a branch the empty asm keeps one (if-converted, each ran for every step
+// behind four v_cndmask per double-double); for a per-lane n the selects measured faster than exec-
+// masked branches (config 3's dominant kernel +1.2 %, profiles/r06u_ab_pow.txt).
+template <bool BR, typename U>
+__device__ __forceinline__ double pow_bin(double x, U n) {
     double bh = x, bl = 0.0;
     while (!(n & 1u)) { // x^(2^k) for the lowest set bit: the result starts there
         dd_sqr(bh, bl);
@@ -208,9 +209,30 @@ __device__ __forceinline__ double pow_libm(double x, double y) {
     double rh = bh, rl = bl;
     while (n >>= 1) {
         dd_sqr(bh, bl);
-        if (n & 1u) dd_mul(rh, rl, bh, bl);
+        if (n & 1u) {
+            if (BR) asm volatile("");
+            dd_mul(rh, rl, bh, bl);
+        }
     }
     return rh + rl;
+}
+// act: the lanes whose result is used.  A wave's records mostly lie on one object: when all of its
+// active lanes share the exponent, the powering runs under scalar control (the exponent read from
+// one lane), with no per-lane loop masks; otherwise each lane loops on its own.  The same operations
+// either way, so the same bits.
+#ifndef RT_POW_UNIFORM
+#define RT_POW_UNIFORM 1
+#endif
+template <bool GENPOW>
+__device__ __forceinline__ double pow_libm(double x, double y, bool act = true) {
+    if (GENPOW && !(y >= 0.0 && y <= 1024.0 && y == __builtin_floor(y))) return pow(x, y);
+    const unsigned n = (unsigned)y;
+#if RT_POW_UNIFORM
+    const unsigned long long am = __ballot(act);
+    const unsigned n0 = (unsigned)__builtin_amdgcn_readlane((int)n, am ? __builtin_ctzll(am) : 0);
+    if (__ballot(act && n != n0) == 0) return n0 == 0 ? 1.0 : pow_bin<true>(x, n0); // (wave-uniform)
+#endif
+    return n == 0 ? 1.0 : pow_bin<false>(x, n);
 }
 
 // ---- primitive tests: return true and t on a valid hit --------------------------------------
@@ -407,7 +429,7 @@ constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIR
 #ifndef RT_DPP_BCAST
 #define RT_DPP_BCAST 0 // 1: measured within noise on configs 3 and 5 (profiles/r06m_ab_dpp_row_bcast.txt)
 #endif
-constexpr int DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143;
+[[maybe_unused]] constexpr int DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143;
 template <int CTRL, int ROWS>
 __device__ __forceinline__ double dpp_f64_rows(double v) {
     const long long b = __double_as_longlong(v);
@@ -545,6 +567,9 @@ __device__ __forceinline__ unsigned long long cull_chunk(const Scene &S, const B
 // single-register DPP reductions) with margins far above binary32 rounding: BEAM32_EPS (1e-5,
 // vs ~1e-6 accumulated relative error in the O(1) cosines and sines), and the positions' rounding
 // (|x| * 2^-24 per coordinate) covered by widening the origin ball by (|origins| + extent) * 1e-6.
+// Their square roots are the hardware's v_sqrt_f32 (sqrt_f32f: within ~1 ulp, 2^-23 relative, far
+// inside those margins) — the correctly rounded sqrtf the compiler emits under IEEE rules is
+// that instruction wrapped in a dozen fix-up operations per call.
 // The axis need not be a unit vector: the cone bounds and the sphere test scale with |axis| alike.
 struct Beam32 {
     float ax, ay, az; // axis (about unit)
@@ -553,27 +578,32 @@ struct Beam32 {
     float ro;         // origin ball radius, position rounding included
     bool on;
 };
-template <int CTRL>
-__device__ __forceinline__ float dpp_f32(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
 __device__ __forceinline__ float lane_f32(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
-template <typename Op>
-__device__ __forceinline__ float wave_reduce32(float v, Op op) {
-    v = op(v, dpp_f32<DPP_XOR1>(v));
-    v = op(v, dpp_f32<DPP_XOR2>(v));
-    v = op(v, dpp_f32<DPP_HALF_MIRROR>(v));
-    v = op(v, dpp_f32<DPP_MIRROR>(v));
-#if RT_DPP_BCAST // (see wave_reduce)
-    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), DPP_ROW_BCAST15, 0xA, 0xF, false)));
-    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), DPP_ROW_BCAST31, 0xC, 0xF, false)));
-    return lane_f32(v, 63);
-#else
-    return op(op(lane_f32(v, 0), lane_f32(v, 16)), op(lane_f32(v, 32), lane_f32(v, 48)));
-#endif
+__device__ __forceinline__ float sqrt_f32f(float x) { return __builtin_amdgcn_sqrtf(x); } // the filters' sqrt
+// Wave minimum / maximum of binary32 values by their bit patterns as signed integers, which order
+// as the values do for every value >= +0 (lengths, radii, extents: the maxima here).  For the
+// minima (the beams' cosine bounds) a negative value anywhere gives some negative result, not
+// necessarily the least, and a negative bound is all the callers test for (the beam is off): the
+// same decisions.  A NaN (positive as an integer) goes into a maximum, where it turns the beam off
+// or keeps every sphere.  Integer min/max need no NaN canonicalisation, so each DPP step is one
+// v_min/max_i32_dpp (bound_ctrl: these four permutations read no invalid lane) and the four rows
+// combine in scalar registers — against a v_mov, a v_mov_dpp and a canonicalising v_max around
+// every fminf / fmaxf step.
+template <bool MAX>
+__device__ __forceinline__ float wave_ext32(float x) {
+    auto op = [](int a, int b) { return MAX ? max(a, b) : min(a, b); };
+    int v = __float_as_int(x);
+    v = op(v, __builtin_amdgcn_mov_dpp(v, DPP_XOR1, 0xF, 0xF, true));
+    v = op(v, __builtin_amdgcn_mov_dpp(v, DPP_XOR2, 0xF, 0xF, true));
+    v = op(v, __builtin_amdgcn_mov_dpp(v, DPP_HALF_MIRROR, 0xF, 0xF, true));
+    v = op(v, __builtin_amdgcn_mov_dpp(v, DPP_MIRROR, 0xF, 0xF, true));
+    return __int_as_float(op(op(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+                             op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48))));
 }
+__device__ __forceinline__ float wave_min32(float x) { return wave_ext32<false>(x); }
+__device__ __forceinline__ float wave_max32(float x) { return wave_ext32<true>(x); }
 // Must be called with the whole wave converged.  o, d: the lanes' ray origins and directions.
 __device__ __forceinline__ Beam32 make_beam32(const SceneHdr &h, bool act, const D3 &o, const D3 &d) {
     Beam32 b;
@@ -593,27 +623,26 @@ __device__ __forceinline__ Beam32 make_beam32(const SceneHdr &h, bool act, const
     const float dd = dx * dx + dy * dy + dz * dz;
     const float cl = ax * dx + ay * dy + az * dz;
     const bool bad = act && !(dd > 1.0f - 0.5f * DIR_TOL && dd < 1.0f + 0.5f * DIR_TOL);
-    const float cmin = wave_reduce32(act ? cl : 2.0f, [](float x, float y) { return fminf(x, y); });
+    const float cmin = wave_min32(act ? cl : 2.0f);
     const float c = cmin - BEAM32_EPS - 2 * DIR_TOL;
     if (__ballot(bad) != 0 || !(c > 0.0f)) return b; // cone wider than a hemisphere: scan everything
     // The sine bound from the cosine bound: every lane has cos >= cmin (to f32 rounding, ~1e-6 with
     // the directions' and the axis' deviation from unit length), so sin^2 = |a|^2 |d|^2 - cos^2 <=
     // 1 + 4 DIR_TOL - cmin^2 (0 < cmin <= 1) — no second reduction (nor the lanes' cross products).
-    const float s = __builtin_sqrtf(fmaxf(1.0f + 4 * DIR_TOL - cmin * cmin, 0.0f)) + BEAM32_EPS + 2 * DIR_TOL;
+    const float s = sqrt_f32f(fmaxf(1.0f + 4 * DIR_TOL - cmin * cmin, 0.0f)) + BEAM32_EPS + 2 * DIR_TOL;
     const int first = __builtin_ctzll(am);
     const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
     b.mx = lane_f32(ox, first);
     b.my = lane_f32(oy, first);
     b.mz = lane_f32(oz, first);
     const float ex = ox - b.mx, ey = oy - b.my, ez = oz - b.mz;
-    const float r2 = wave_reduce32(act ? ex * ex + ey * ey + ez * ez : 0.0f, [](float x, float y) { return fmaxf(x, y); });
+    const float r2 = wave_max32(act ? ex * ex + ey * ey + ez * ez : 0.0f);
     // the origins' extent in binary32 (|o| rounded to nearest: within 2^-24 relative, far inside the
     // 1e-6 margin below; the extent check keeps a 1e-6 relative slack for it)
-    const float mo = wave_reduce32(act ? fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz))) : 0.0f,
-                                   [](float x, float y) { return fmaxf(x, y); });
+    const float mo = wave_max32(act ? fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz))) : 0.0f);
     if (!(mo <= (float)(CULL_EXTENT * (1.0 - 1.0e-6)))) return b;
     b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
-    b.ro = __builtin_sqrtf(r2) * (1.0f + BEAM32_EPS) + BEAM32_EPS + (mo + (float)h.ext) * 1.0e-6f;
+    b.ro = sqrt_f32f(r2) * (1.0f + BEAM32_EPS) + BEAM32_EPS + (mo + (float)h.ext) * 1.0e-6f;
     b.on = true;
     return b;
 }
@@ -628,10 +657,10 @@ __device__ __forceinline__ unsigned long long cull_chunk32(const Scene &S, const
                                 : reinterpret_cast<const double2 *>(S.tab + h.o_sph_b + kk * SPH_B_W);
     const double2 g01 = g[0], g23 = g[1];
     const float vx = (float)g01.x - b.mx, vy = (float)g01.y - b.my, vz = (float)g23.x - b.mz;
-    const float vl = __builtin_sqrtf(vx * vx + vy * vy + vz * vz);
+    const float vl = sqrt_f32f(vx * vx + vy * vy + vz * vz);
     const float rp = (float)g23.y + b.ro;
     const float sr = rp * __builtin_amdgcn_rcpf(vl) * (1.0f + BEAM32_EPS) + BEAM32_EPS;
-    const float cr = __builtin_sqrtf(fmaxf(1.0f - sr * sr, 0.0f)) - BEAM32_EPS;
+    const float cr = sqrt_f32f(fmaxf(1.0f - sr * sr, 0.0f)) - BEAM32_EPS;
     const float thr = b.c * cr - b.s * sr;
     const float av = b.ax * vx + b.ay * vy + b.az * vz;
     const bool keep = (vl <= rp * (1.0f + BEAM32_EPS) + BEAM32_EPS) | (sr >= 1.0f) | !(av + BEAM32_EPS * vl < thr * vl);
@@ -688,10 +717,10 @@ __device__ __forceinline__ Beam32 make_beam_pair32(const SceneHdr &h, bool a0, c
     float cl0, cl1;
     const bool bad0 = lane_terms(a0, x0, y0, z0, cl0); // both sets evaluated (no short circuit)
     const bool bad1 = lane_terms(a1, x1, y1, z1, cl1);
-    const float cmin = wave_reduce32(fminf(a0 ? cl0 : 2.0f, a1 ? cl1 : 2.0f), [](float x, float y) { return fminf(x, y); });
+    const float cmin = wave_min32(fminf(a0 ? cl0 : 2.0f, a1 ? cl1 : 2.0f));
     const float c = cmin - BEAM32_EPS - 2 * DIR_TOL;
     if (__ballot(bad0 || bad1) != 0 || !(c > 0.0f)) return b;
-    const float s = __builtin_sqrtf(fmaxf(1.0f + 4 * DIR_TOL - cmin * cmin, 0.0f)) + BEAM32_EPS + 2 * DIR_TOL; // make_beam32
+    const float s = sqrt_f32f(fmaxf(1.0f + 4 * DIR_TOL - cmin * cmin, 0.0f)) + BEAM32_EPS + 2 * DIR_TOL; // make_beam32
     b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
     b.on = true;
     return b;
@@ -1199,7 +1228,7 @@ __device__ __forceinline__ Target make_target(const Scene &S, int obj, bool acti
 // exactly, and it is the same binary32 comparison on both sides (rt_scene.cpp).
 __device__ __forceinline__ int occ_cell(const double *q, const D3 &sd) {
     const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
-    const float D = __builtin_sqrtf(qx * qx + qy * qy + qz * qz);
+    const float D = sqrt_f32f(qx * qx + qy * qy + qz * qz); // (a filter: cells overlap by OCC_CELL_EPS)
     const float ax = __builtin_fabsf(qx), ay = __builtin_fabsf(qy), az = __builtin_fabsf(qz);
     const int drop = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
     const float ex = (float)sd.x * D + qx, ey = (float)sd.y * D + qy, ez = (float)sd.z * D + qz;
@@ -1384,7 +1413,7 @@ __device__ __forceinline__ D3 shade(const Scene &S, int id, const D3 &d, const D
         const D3 diff = {mc.x * dd, mc.y * dd, mc.z * dd};
         // specular_term/7 (:285-297)
         const D3 hn = normalize3(D3{ln.x + -d.x, ln.y + -d.y, ln.z + -d.z});
-        const double sp = shin * pow_libm<GENPOW>(max0(dot3(hn, N)), spow);
+        const double sp = shin * pow_libm<GENPOW>(max0(dot3(hn, N)), spow, active);
         const D3 spec = {Sc.x * sp, Sc.y * sp, Sc.z * sp};
         const D3 con = {diff.x + spec.x, diff.y + spec.y, diff.z + spec.z};
         // A lane whose light term Lc (x) con is exactly zero gets the same bits for lit = 0 and

@@ -8,6 +8,7 @@
 #   bash scripts/gpu_r06.sh TAG setup     config 3 lines with the setup leg (8 and 4 HW queues), config 5's, the N = 8 floor
 #   bash scripts/gpu_r06.sh TAG prof3     rocprofv3 kernel trace + PMC passes of config 3
 #   bash scripts/gpu_r06.sh TAG prof5     the same for config 5 (prof2: config 2)
+#   VARIANTS="- a b" [PMCV_ARGS=...] bash scripts/gpu_r06.sh TAG pmcv   instruction counts per kernel of variants
 set -o pipefail
 TAG=${1:-r06}
 PART=${2:-test}
@@ -71,6 +72,16 @@ prof3)
   bash scripts/profile.sh prof_${TAG}_c3 > gpurun_out/prof_${TAG}_c3.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_c3.log; exit 1; }
   python3 scripts/pmc_summary.py gpurun_out/prof_${TAG}_c3 gpurun_out/${TAG}_c3_pmc.json s64-4096x4096-d5-exact-f32-n1 20 20 > gpurun_out/${TAG}_c3_pmc.txt || exit 1
   grep -E "window_ns|f64_issue|wait_any_share|hbm_bytes" gpurun_out/${TAG}_c3_pmc.txt ;;
+pmcv)
+  # instruction counts per kernel of library variants (VARIANTS as for ab; PMCV_ARGS: bench.py arguments)
+  for v in ${VARIANTS:--}; do
+    lib=""; [ "$v" = "-" ] || lib="eraytracer_amd/variants/librtmi355x_$v.so"
+    RT_LIB_PATH=$lib timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_BRANCH \
+      -d gpurun_out/pmcv_$TAG/$v -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --iso 0 --settle 0 --no-cpu-baseline --no-boundary --no-setup ${PMCV_ARGS:-} > gpurun_out/pmcv_${TAG}_$v.log 2>&1 || { tail -5 gpurun_out/pmcv_${TAG}_$v.log; exit 1; }
+  done
+  python3 scripts/pmc_variants.py gpurun_out/pmcv_$TAG > gpurun_out/pmcv_$TAG.txt || exit 1
+  tail -8 gpurun_out/pmcv_$TAG.txt
+  rm -rf gpurun_out/pmcv_$TAG ;;
 prof2)
   bash scripts/profile.sh prof_${TAG}_c2 $C2 > gpurun_out/prof_${TAG}_c2.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_c2.log; exit 1; }
   python3 scripts/pmc_summary.py gpurun_out/prof_${TAG}_c2 gpurun_out/${TAG}_c2_pmc.json default-1920x1080-d5-exact-f32-n1 20 20 > gpurun_out/${TAG}_c2_pmc.txt || exit 1
