@@ -280,7 +280,9 @@ __device__ __forceinline__ bool sph_t_wave(double B, double C, double A4, double
     const bool ok = disc >= 0.001;
     t = 0.0;
     if (__ballot(ok) == 0) return false;
-    const double sq = sqrt_x<FAST>(ok ? disc : 1.0);
+    // FAST: the failing lanes' roots (NaN for disc < 0) are dropped by `ok` below; only the range-checked
+    // form needs them in range, lest they send the wave down the full sqrt
+    const double sq = sqrt_x<FAST>(FAST || ok ? disc : 1.0);
     t = (-B - sq) / 2; // the nearer root (sph_t)
     return ok & (t >= 0);
 }
@@ -605,6 +607,12 @@ __device__ __forceinline__ float wave_ext32(float x) {
 __device__ __forceinline__ float wave_min32(float x) { return wave_ext32<false>(x); }
 __device__ __forceinline__ float wave_max32(float x) { return wave_ext32<true>(x); }
 // Must be called with the whole wave converged.  o, d: the lanes' ray origins and directions.
+// SPHO: a spheres-only scene's reflection rays — every origin is a hit point on a sphere, so its
+// coordinates are within 2 h.ext (h.ext bounds |centre| and |radius| alike; the binary64 hit point's
+// rounding is ~1e-16 of that), which replaces the wave maximum of |origin|; and every direction is a
+// reflection off a normalised sphere normal of a normalised ray, of unit length to ~1e-15 per level,
+// so the DIR_TOL check (which catches the reflections off planes with non-unit normals) cannot fail.
+template <bool SPHO = false>
 __device__ __forceinline__ Beam32 make_beam32(const SceneHdr &h, bool act, const D3 &o, const D3 &d) {
     Beam32 b;
     b.on = false;
@@ -622,7 +630,7 @@ __device__ __forceinline__ Beam32 make_beam32(const SceneHdr &h, bool act, const
     constexpr float DIR_TOL = 1.0e-6f;
     const float dd = dx * dx + dy * dy + dz * dz;
     const float cl = ax * dx + ay * dy + az * dz;
-    const bool bad = act && !(dd > 1.0f - 0.5f * DIR_TOL && dd < 1.0f + 0.5f * DIR_TOL);
+    const bool bad = !SPHO && act && !(dd > 1.0f - 0.5f * DIR_TOL && dd < 1.0f + 0.5f * DIR_TOL);
     const float cmin = wave_min32(act ? cl : 2.0f);
     const float c = cmin - BEAM32_EPS - 2 * DIR_TOL;
     if (__ballot(bad) != 0 || !(c > 0.0f)) return b; // cone wider than a hemisphere: scan everything
@@ -639,7 +647,8 @@ __device__ __forceinline__ Beam32 make_beam32(const SceneHdr &h, bool act, const
     const float r2 = wave_max32(act ? ex * ex + ey * ey + ez * ez : 0.0f);
     // the origins' extent in binary32 (|o| rounded to nearest: within 2^-24 relative, far inside the
     // 1e-6 margin below; the extent check keeps a 1e-6 relative slack for it)
-    const float mo = wave_max32(act ? fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz))) : 0.0f);
+    const float mo = SPHO ? (float)(2.0 * h.ext) * (1.0f + 1.0e-6f)
+                          : wave_max32(act ? fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz))) : 0.0f);
     if (!(mo <= (float)(CULL_EXTENT * (1.0 - 1.0e-6)))) return b;
     b.ax = ax; b.ay = ay; b.az = az; b.c = c; b.s = s;
     b.ro = sqrt_f32f(r2) * (1.0f + BEAM32_EPS) + BEAM32_EPS + (mo + (float)h.ext) * 1.0e-6f;
@@ -784,7 +793,7 @@ __device__ __forceinline__ void scan_spheres(const Scene &S, int org, const D3 &
         const double disc0 = B0 * B0 - A4 * C0, disc1 = B1 * B1 - A4 * C1;
         const bool ok0 = disc0 >= 0.001, ok1 = disc1 >= 0.001;
         if (__ballot(ok0 | ok1) == 0) continue;
-        const double sq0 = sqrt_x<FAST>(ok0 ? disc0 : 1.0), sq1 = sqrt_x<FAST>(ok1 ? disc1 : 1.0);
+        const double sq0 = sqrt_x<FAST>(FAST || ok0 ? disc0 : 1.0), sq1 = sqrt_x<FAST>(FAST || ok1 ? disc1 : 1.0); // (sph_t_wave)
         const double t0 = (-B0 - sq0) / 2, t1 = (-B1 - sq1) / 2; // the nearer roots (sph_t)
         const bool h0 = ok0 & (t0 >= 0), h1 = two & ok1 & (t1 >= 0);
         const bool u0 = h0 & nearer(t0, id0, bt, bid);
@@ -1035,7 +1044,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
             const int gv = __builtin_amdgcn_readlane(grp, __builtin_ctzll(rem));
             const bool sel = (g == MAX_GROUPS - 1) ? ((rem >> (threadIdx.x & 63)) & 1) != 0 : (act && grp == gv);
             rem &= ~__ballot(sel);
-            const Beam32 b = make_beam32(h, sel, o, d);
+            const Beam32 b = make_beam32<(SPH >= 1)>(h, sel, o, d);
             RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
             if (!b.on) {
                 all = true;
@@ -1067,7 +1076,7 @@ __device__ __forceinline__ int nearest(const Scene &S, int org, const D3 &o, con
                 scan_spheres<PRE, ILP, (SPH >= 1)>(S, org, o, d, A4, chunk, m, bt, bid);
             }
         } else {
-            const Beam32 b = make_beam32(h, sel, o, d);
+            const Beam32 b = make_beam32<(SPH >= 1)>(h, sel, o, d);
             on = b.on;
             RT_STAT(ST_BEAM_ON, b.on ? 1 : 0);
             for (int chunk = 0; chunk < h.n_sph; chunk += 64) {
