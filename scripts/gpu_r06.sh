@@ -39,6 +39,19 @@ ab)
       done
     done
   done ;;
+envab)
+  # A/B of run-time knobs: ENVS="- RT_BVH_LEVEL=3 ..." (each item one VAR=value, or - for none)
+  : > gpurun_out/${TAG}_envab.txt
+  for rep in $(seq 1 ${REPS:-2}); do
+    for c in ${CFGS:-c3dq c5q}; do
+      for e in ${ENVS:--}; do
+        ev=""; [ "$e" = "-" ] || ev="$e"
+        env $ev timeout -k 10 300 python bench.py $(cfg_args $c) > gpurun_out/${TAG}_envab_one.json 2> gpurun_out/${TAG}_envab_one.err \
+          || { tail -5 gpurun_out/${TAG}_envab_one.err; exit 1; }
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d.get('roofline',{}); print(sys.argv[2], d['value'], 'Mpx/s', d['ms_per_step'], 'ms/frame', 'dom', r.get('launch_ms_live'))" gpurun_out/${TAG}_envab_one.json "$c $e rep$rep" | tee -a gpurun_out/${TAG}_envab.txt || exit 1
+      done
+    done
+  done ;;
 lim)
   make -C oracle > /dev/null || exit 1
   timeout -k 10 900 python -u -m pytest tests/test_gpu_limits.py -x -v -m gpu --timeout 400 --timeout-method thread > gpurun_out/pytest_lim_$TAG.log 2>&1 || { tail -40 gpurun_out/pytest_lim_$TAG.log; exit 1; }
