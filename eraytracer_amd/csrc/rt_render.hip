@@ -1590,7 +1590,8 @@ __global__ __launch_bounds__(256, NB ? RT_FUSED_NB_WAVES : RT_WAVES_PER_SIMD) vo
 #include "rt_wave.inc" // the wavefront engine (default)
 
 // rt_selftest_math: sqrt_n / div_n against the device library's sqrt and division, bit for bit,
-// on operands spread log-uniformly over the ranges where the kernels use them.
+// on operands spread log-uniformly over the ranges where the kernels use them; pow_libm's wave-
+// uniform path against the per-lane powering; the binary32 wave reductions against a lane loop.
 __global__ __launch_bounds__(256) void k_selftest_math(unsigned long long n, unsigned long long seed,
                                                        unsigned long long *__restrict__ bad) {
     unsigned long long local = 0;
@@ -1629,6 +1630,33 @@ __global__ __launch_bounds__(256) void k_selftest_math(unsigned long long n, uns
                        __double_as_longlong(u.y) != __double_as_longlong(v.y * sc) ||
                        __double_as_longlong(u.z) != __double_as_longlong(v.z * sc)))
             ++local;
+        // pow_libm's scalar-controlled powering (a wave-uniform exponent: one per 64 consecutive i,
+        // every other group) against the per-lane powering, bit for bit; x over [0, 1 + 2^-20)
+        {
+            const double px = (double)(r2 & 0xFFFFFFFFFFFull) * 0x1p-44 * (1.0 + 0x1p-20);
+            const unsigned pu = (unsigned)(splitmix64(seed ^ (i >> 6)) % 1025u), pl = (unsigned)((r2 >> 44) % 1025u);
+            const unsigned pn = ((i >> 6) & 1) ? pu : pl;
+            const double want = pn == 0 ? 1.0 : pow_bin<false>(px, pn);
+            if (__double_as_longlong(pow_libm<false>(px, (double)pn)) != __double_as_longlong(want)) ++local;
+        }
+        // the binary32 wave reductions (whole waves only): the maximum of values >= +0 exactly, the
+        // minimum exactly when no value is negative and negative when one is
+        if (__ballot(true) == ~0ull) {
+            const float f0 = (float)((double)(r & 0xFFFFFF) * 0x1p-20);
+            const float fv = (r >> 40) % 97 == 0 ? -1.0f - f0 : f0; // (no -0.0: its bits order below +0.0's)
+            const float fa = __builtin_fabsf(fv);
+            float tmin = 3.0e38f, tmax = 0.0f;
+            bool neg = false;
+            for (int l = 0; l < 64; ++l) { // (wave-uniform)
+                const float a = lane_f32(fv, l), b = lane_f32(fa, l);
+                tmin = a < tmin ? a : tmin;
+                tmax = b > tmax ? b : tmax;
+                neg = neg || a < 0.0f;
+            }
+            const float gmin = wave_min32(fv), gmax = wave_max32(fa);
+            if (__float_as_int(gmax) != __float_as_int(tmax) || (neg ? !(gmin < 0.0f) : __float_as_int(gmin) != __float_as_int(tmin)))
+                ++local;
+        }
     }
     if (local) atomicAdd(bad, local);
 }

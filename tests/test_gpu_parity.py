@@ -525,7 +525,9 @@ def test_frames_in_flight_match_single_frame():
 
 def test_fast_sqrt_and_division_are_the_library_bits():
     """sqrt_n / div_n / normalize3 (the kernels' range-guarded fast paths) against the device
-    library's sqrt and division on 2^26 random operands each: no bit differs."""
+    library's sqrt and division on 2^26 random operands each: no bit differs.  The same kernel checks
+    pow_libm's scalar-controlled powering (wave-uniform exponents) against the per-lane powering, bit
+    for bit, and the binary32 beams' integer-order wave reductions against a lane-by-lane loop."""
     bad = ctypes.c_uint64(123)
     N.check(N.lib().rt_selftest_math(0, 1 << 26, 0x5EED, ctypes.byref(bad)), "rt_selftest_math")
     assert bad.value == 0
