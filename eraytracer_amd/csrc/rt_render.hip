@@ -590,9 +590,10 @@ __device__ __forceinline__ float sqrt_f32f(float x) { return __builtin_amdgcn_sq
 // necessarily the least, and a negative bound is all the callers test for (the beam is off): the
 // same decisions.  A NaN (positive as an integer) goes into a maximum, where it turns the beam off
 // or keeps every sphere.  Integer min/max need no NaN canonicalisation, so each DPP step is one
-// v_min/max_i32_dpp (bound_ctrl: these four permutations read no invalid lane) and the four rows
-// combine in scalar registers — against a v_mov, a v_mov_dpp and a canonicalising v_max around
-// every fminf / fmaxf step.
+// v_min/max_i32_dpp (bound_ctrl: these four permutations read no invalid lane), and the four rows'
+// results are read and combined — against a v_mov, a v_mov_dpp and a canonicalising v_max around
+// every fminf / fmaxf step.  (Combining them with s_min/s_max in inline asm measured slower:
+// profiles/r06ab_ab_salu_bvh_knobs.txt.)
 template <bool MAX>
 __device__ __forceinline__ float wave_ext32(float x) {
     auto op = [](int a, int b) { return MAX ? max(a, b) : min(a, b); };
