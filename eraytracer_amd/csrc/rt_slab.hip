@@ -176,53 +176,71 @@ __global__ __launch_bounds__(SLAB_BLOCK) void k_unpack(ShardPtrs sp, uint64_t ma
 }
 
 // Frames whose width is a multiple of 4: each thread decodes 4 consecutive pixels of an image row
-// (their mask bits share one word: p is a multiple of 4) and writes them as 16-byte stores (48 B of
-// binary32 RGB, 96 of binary64), one workgroup per (row, 1024 columns).  The frame is the bulk of
-// the decode's traffic (201 MB at 4096^2 f32 against ~55 MB of values for S64), so wide stores and a
-// quarter of the threads' rank computations are what its speed rests on (scripts/n8_floor.py).
+// (their mask bits share one word: p is a multiple of 4), one workgroup per (row, 1024 columns).
+// The frame is the bulk of the decode's traffic (201 MB at 4096^2 f32 against ~55 MB of values
+// for S64), so the stores decide its speed: each thread's 3 (binary32) or 6 (binary64) 16-byte
+// pieces are staged in LDS and the workgroup writes its contiguous stretch of the frame with lane i
+// of a store instruction at 16 i bytes (1 KiB per wave instruction instead of 16 B every 48 B),
+// non-temporal (the frame is not read back on the device).  4096^2 f32, 8 shards: 0.068 -> 0.035 ms,
+// 7.4 TB/s of algorithmic bytes (profiles/r06aj_codec_ab.txt).
 constexpr int UNPACK_PX = 4;
 template <typename T>
 __global__ __launch_bounds__(SLAB_BLOCK) void k_unpack4(ShardPtrs sp, uint64_t mask_at, uint64_t px, uint32_t W,
-                                                        uint32_t ncol, uint32_t rb, uint32_t ns, T *__restrict__ image) {
+                                                         uint32_t ncol, uint32_t rb, uint32_t ns, T *__restrict__ image) {
+    constexpr int Q = 3 * UNPACK_PX * (int)sizeof(T) / 16; // 16-byte pieces per thread
+    __shared__ uint4 s_out[SLAB_BLOCK * Q];
     const uint32_t g = blockIdx.x / ncol, c = blockIdx.x - g * ncol;
-    const uint32_t x = (c * SLAB_BLOCK + threadIdx.x) * UNPACK_PX;
-    if (x >= W) return;
-    const uint32_t blk = g / rb, s = blk % ns;
-    const uint64_t lr = (uint64_t)(blk / ns) * rb + (g - blk * rb);
-    const uint64_t p = lr * W + x; // a multiple of 4 (W is)
-    const unsigned char *h = sp.hdr[s];
-    const uint32_t *off = reinterpret_cast<const uint32_t *>(h + HDR_OFFS);
-    const uint64_t *mask = reinterpret_cast<const uint64_t *>(h + mask_at);
-    const unsigned bits = (unsigned)(mask[p / 64] >> (p % 64)) & 0xFu;
-    T v[3 * UNPACK_PX];
+    const uint32_t x0 = c * SLAB_BLOCK * UNPACK_PX, x = x0 + threadIdx.x * UNPACK_PX;
+    const uint32_t nact = (W - x0 < SLAB_BLOCK * UNPACK_PX ? W - x0 : SLAB_BLOCK * UNPACK_PX) / UNPACK_PX;
+    if (x < W) {
+        const uint32_t blk = g / rb, s = blk % ns;
+        const uint64_t lr = (uint64_t)(blk / ns) * rb + (g - blk * rb);
+        const uint64_t p = lr * W + x; // a multiple of 4 (W is)
+        const unsigned char *h = sp.hdr[s];
+        const uint32_t *off = reinterpret_cast<const uint32_t *>(h + HDR_OFFS);
+        const uint64_t *mask = reinterpret_cast<const uint64_t *>(h + mask_at);
+        const unsigned bits = (unsigned)(mask[p / 64] >> (p % 64)) & 0xFu;
+        T v[3 * UNPACK_PX];
 #pragma unroll
-    for (int k = 0; k < 3 * UNPACK_PX; ++k) v[k] = 0;
-    if (bits) {
-        uint64_t r = rank_of(off, mask, p);
-        if (r + __popc(bits) <= px) { // (a consistent header never ranks past the slab)
-            const T *src = static_cast<const T *>(sp.vals[s]);
+        for (int k = 0; k < 3 * UNPACK_PX; ++k) v[k] = 0;
+        if (bits) {
+            uint64_t r = rank_of(off, mask, p);
+            if (r + __popc(bits) <= px) { // (a consistent header never ranks past the slab)
+                const T *src = static_cast<const T *>(sp.vals[s]);
 #pragma unroll
-            for (int k = 0; k < UNPACK_PX; ++k) {
-                if ((bits >> k) & 1u) {
-                    v[3 * k] = src[r * 3];
-                    v[3 * k + 1] = src[r * 3 + 1];
-                    v[3 * k + 2] = src[r * 3 + 2];
-                    ++r;
+                for (int k = 0; k < UNPACK_PX; ++k) {
+                    if ((bits >> k) & 1u) {
+                        v[3 * k] = src[r * 3];
+                        v[3 * k + 1] = src[r * 3 + 1];
+                        v[3 * k + 2] = src[r * 3 + 2];
+                        ++r;
+                    }
                 }
             }
         }
+        uint4 *so = s_out + threadIdx.x * Q;
+        if constexpr (sizeof(T) == 4) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                so[k] = make_uint4((unsigned)v[4 * k], (unsigned)v[4 * k + 1], (unsigned)v[4 * k + 2], (unsigned)v[4 * k + 3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                so[k] = make_uint4((unsigned)v[2 * k], (unsigned)(v[2 * k] >> 32), (unsigned)v[2 * k + 1],
+                                   (unsigned)(v[2 * k + 1] >> 32));
+        }
     }
-    // 16-byte aligned: ((g * W + x) * 3 * sizeof(T)) is a multiple of 48 (x and W multiples of 4)
-    uint4 *o = reinterpret_cast<uint4 *>(image + ((uint64_t)g * W + x) * 3);
-    if constexpr (sizeof(T) == 4) {
+    __syncthreads();
+    uint4 *o = reinterpret_cast<uint4 *>(image + ((uint64_t)g * W + x0) * 3);
+    const uint32_t n16 = nact * Q;
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-            o[k] = make_uint4((unsigned)v[4 * k], (unsigned)v[4 * k + 1], (unsigned)v[4 * k + 2], (unsigned)v[4 * k + 3]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 6; ++k)
-            o[k] = make_uint4((unsigned)v[2 * k], (unsigned)(v[2 * k] >> 32), (unsigned)v[2 * k + 1],
-                              (unsigned)(v[2 * k + 1] >> 32));
+    for (int k = 0; k < Q; ++k) {
+        const uint32_t i = k * SLAB_BLOCK + threadIdx.x;
+        if (i < n16) {
+            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+            const uint4 w = s_out[i];
+            __builtin_nontemporal_store(v4u{w.x, w.y, w.z, w.w}, reinterpret_cast<v4u *>(o + i));
+        }
     }
 }
 
@@ -293,11 +311,11 @@ int rt_slab_unpack(const void *const *d_headers, const void *const *d_values, ui
         const uint64_t nblocks = (uint64_t)ncol * height;
         if (nblocks >= (1ull << 31)) return RT_ETOOBIG;
         if (precision == RT_OUT_F32)
-            hipLaunchKernelGGL(k_unpack4<uint32_t>, dim3((unsigned)nblocks), dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, l.px,
-                               width, ncol, row_block, nshards, static_cast<uint32_t *>(d_image));
+            hipLaunchKernelGGL(k_unpack4<uint32_t>, dim3((unsigned)nblocks), dim3(SLAB_BLOCK), 0, st, sp, l.mask_at,
+                               l.px, width, ncol, row_block, nshards, static_cast<uint32_t *>(d_image));
         else
-            hipLaunchKernelGGL(k_unpack4<uint64_t>, dim3((unsigned)nblocks), dim3(SLAB_BLOCK), 0, st, sp, l.mask_at, l.px,
-                               width, ncol, row_block, nshards, static_cast<uint64_t *>(d_image));
+            hipLaunchKernelGGL(k_unpack4<uint64_t>, dim3((unsigned)nblocks), dim3(SLAB_BLOCK), 0, st, sp, l.mask_at,
+                               l.px, width, ncol, row_block, nshards, static_cast<uint64_t *>(d_image));
         SLABCHK(hipGetLastError());
         return RT_OK;
     }
